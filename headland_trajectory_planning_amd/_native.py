@@ -1,0 +1,231 @@
+"""ctypes binding of libhtp.so (include/htp.h) and batch packing.
+
+The product path REQUIRES the in-tree HIP library: `load()` raises if it is
+missing -- there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhtp.so")
+NPARAM = 24
+(P_DT, P_Q00, P_Q01, P_Q10, P_Q11, P_R00, P_R01, P_R10, P_R11, P_W00, P_W11, P_WHEELBASE, P_MAXSTEER,
+ P_MAXV, P_MAXACC, P_MAXSR, P_DMIN, P_XLO, P_XHI, P_YLO, P_YHI, P_HAS_INIT_CONTROL, P_HAS_INIT_DUAL) = range(23)
+
+STATUS_STR = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Maximum_Iterations_Exceeded",
+              3: "Restoration_Failed", 4: "Error_In_Step_Computation", 5: "Invalid_Problem_Definition"}
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int32)
+
+
+class ObcaBatch(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("N", ctypes.c_int32), ("M", ctypes.c_int32), ("K", ctypes.c_int32),
+                ("time_opt", ctypes.c_int32), ("obs_edges", ctypes.c_void_p), ("body_edges", ctypes.c_void_p),
+                ("traj", ctypes.c_void_p), ("obs_A", ctypes.c_void_p), ("obs_b", ctypes.c_void_p),
+                ("body_G", ctypes.c_void_p), ("body_g", ctypes.c_void_p), ("params", ctypes.c_void_p),
+                ("init_control", ctypes.c_void_p), ("init_mu", ctypes.c_void_p), ("init_lambda", ctypes.c_void_p)]
+
+
+class ObcaResult(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_void_p), ("objective", ctypes.c_void_p), ("status", ctypes.c_void_p),
+                ("iterations", ctypes.c_void_p), ("n_factor", ctypes.c_void_p), ("nlp_error", ctypes.c_void_p)]
+
+
+EXPORTS = ["htp_obca_sizes", "htp_create", "htp_destroy", "htp_last_error", "htp_set_option",
+           "htp_obca_solve_batch", "htp_obca_solve_batch_device", "htp_last_kernel_ms"]
+
+
+def _declare(lib):
+    lib.htp_obca_sizes.argtypes = [ctypes.c_int32] * 4 + [ctypes.c_void_p] * 2 + [ctypes.POINTER(ctypes.c_int64)] * 4
+    lib.htp_obca_sizes.restype = ctypes.c_int
+    lib.htp_create.argtypes = [ctypes.c_int32]
+    lib.htp_create.restype = ctypes.c_void_p
+    lib.htp_destroy.argtypes = [ctypes.c_void_p]
+    lib.htp_destroy.restype = None
+    lib.htp_last_error.argtypes = [ctypes.c_void_p]
+    lib.htp_last_error.restype = ctypes.c_char_p
+    lib.htp_set_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_double]
+    lib.htp_set_option.restype = ctypes.c_int
+    lib.htp_obca_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ObcaBatch), ctypes.POINTER(ObcaResult)]
+    lib.htp_obca_solve_batch.restype = ctypes.c_int
+    lib.htp_obca_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ObcaBatch),
+                                                ctypes.POINTER(ObcaResult), ctypes.c_void_p]
+    lib.htp_obca_solve_batch_device.restype = ctypes.c_int
+    lib.htp_last_kernel_ms.argtypes = [ctypes.c_void_p]
+    lib.htp_last_kernel_ms.restype = ctypes.c_double
+    return lib
+
+
+_LIB = None
+
+
+def load(path=LIB_PATH):
+    """Load the in-tree HIP library; raise loudly if it is absent."""
+    global _LIB
+    if _LIB is not None and path == LIB_PATH:
+        return _LIB
+    if not os.path.exists(path):
+        raise RuntimeError(f"[htp] HIP library not built: {path} (run __graft_entry__.build())")
+    lib = _declare(ctypes.CDLL(path))
+    if path == LIB_PATH:
+        _LIB = lib
+    return lib
+
+
+def sizes(N, M, K, time_opt, obs_edges, body_edges, lib=None):
+    lib = lib or load()
+    eo = np.ascontiguousarray(obs_edges, dtype=np.int32)
+    eb = np.ascontiguousarray(body_edges, dtype=np.int32)
+    out = [ctypes.c_int64() for _ in range(4)]
+    rc = lib.htp_obca_sizes(N, M, K, int(time_opt), eo.ctypes.data, eb.ctypes.data, *[ctypes.byref(v) for v in out])
+    if rc != 0:
+        raise ValueError("[OBCA] invalid problem shape")
+    return tuple(v.value for v in out)
+
+
+# ------------------------------------------------------------------ packing
+def params_of(inst):
+    p = np.zeros(NPARAM)
+    Q, R, W = (np.asarray(inst[k], dtype=np.float64) for k in ("Q", "R", "W"))
+    p[P_DT] = inst["dT"]
+    p[P_Q00:P_Q11 + 1] = Q.reshape(-1)[:4]
+    p[P_R00:P_R11 + 1] = R.reshape(-1)[:4]
+    p[P_W00], p[P_W11] = W[0, 0], W[1, 1]
+    p[P_WHEELBASE] = inst["wheelbase"]
+    p[P_MAXSTEER] = inst["max_steer"]
+    p[P_MAXV] = inst["max_velocity"]
+    p[P_MAXACC] = inst["max_accel"]
+    p[P_MAXSR] = inst["max_steer_rate"]
+    dmin = inst.get("min_dist", 0.1)
+    p[P_DMIN] = 0.1 if (dmin is None or dmin < 0) else dmin
+    xb = inst.get("x_bound", [-np.inf, np.inf])
+    yb = inst.get("y_bound", [-np.inf, np.inf])
+    p[P_XLO], p[P_XHI], p[P_YLO], p[P_YHI] = xb[0], xb[1], yb[0], yb[1]
+    p[P_HAS_INIT_CONTROL] = inst.get("init_control") is not None
+    p[P_HAS_INIT_DUAL] = inst.get("init_mu") is not None
+    return p
+
+
+class PackedBatch:
+    """Contiguous problem-major arrays for one batch (shared shape)."""
+
+    def __init__(self, insts):
+        i0 = insts[0]
+        self.batch = len(insts)
+        self.N = int(np.asarray(i0["init_traj"]).shape[0])
+        self.M = len(i0["obs_A"])
+        self.K = len(i0["body_G"])
+        self.time_opt = int(np.asarray(i0["W"])[1, 1] != 0)
+        self.obs_edges = np.array([a.shape[0] for a in i0["obs_A"]], dtype=np.int32)
+        self.body_edges = np.array([a.shape[0] for a in i0["body_G"]], dtype=np.int32)
+        for it in insts:
+            if (np.asarray(it["init_traj"]).shape[0] != self.N
+                    or [a.shape[0] for a in it["obs_A"]] != list(self.obs_edges)
+                    or [a.shape[0] for a in it["body_G"]] != list(self.body_edges)
+                    or int(np.asarray(it["W"])[1, 1] != 0) != self.time_opt):
+                raise ValueError("[OBCA] all problems of a batch must share N, edge counts and time_opt")
+        B = self.batch
+        self.traj = np.ascontiguousarray(np.stack([np.asarray(it["init_traj"], dtype=np.float64) for it in insts]))
+        self.obs_A = np.ascontiguousarray(np.stack([np.concatenate(it["obs_A"], axis=0) for it in insts]))
+        self.obs_b = np.ascontiguousarray(np.stack([np.concatenate(it["obs_b"]) for it in insts]))
+        self.body_G = np.ascontiguousarray(np.stack([np.concatenate(it["body_G"], axis=0) for it in insts]))
+        self.body_g = np.ascontiguousarray(np.stack([np.concatenate(it["body_g"]) for it in insts]))
+        self.params = np.ascontiguousarray(np.stack([params_of(it) for it in insts]))
+        self.init_control = self._opt(insts, "init_control")
+        self.init_mu = self._opt(insts, "init_mu")
+        self.init_lambda = self._opt(insts, "init_lambda")
+        TEo, TEb = int(self.obs_edges.sum()), int(self.body_edges.sum())
+        self.mu_count, self.lam_count = TEb * self.M, TEo * self.K
+        self.n_var = 5 * self.N + 2 * (self.N - 1) + self.N * (self.mu_count + self.lam_count) + \
+            (self.N - 1) * self.time_opt + 5
+        _ = B
+
+    @staticmethod
+    def _opt(insts, key):
+        vals = [it.get(key) for it in insts]
+        if all(v is None for v in vals):
+            return None
+        if any(v is None for v in vals):
+            raise ValueError(f"[OBCA] {key} must be given for all or none of the problems")
+        return np.ascontiguousarray(np.stack([np.asarray(v, dtype=np.float64) for v in vals]))
+
+    def struct(self, ptrs=None):
+        """ctypes htp_obca_batch over host arrays (or the given device pointers)."""
+        def ptr(a):
+            return None if a is None else a.ctypes.data
+        b = ObcaBatch()
+        b.batch, b.N, b.M, b.K, b.time_opt = self.batch, self.N, self.M, self.K, self.time_opt
+        b.obs_edges, b.body_edges = self.obs_edges.ctypes.data, self.body_edges.ctypes.data
+        src = ptrs or {}
+        for name in ("traj", "obs_A", "obs_b", "body_G", "body_g", "params", "init_control", "init_mu", "init_lambda"):
+            setattr(b, name, src[name] if name in src else ptr(getattr(self, name)))
+        return b
+
+
+class HostResults:
+    def __init__(self, batch, n_var):
+        self.x = np.zeros((batch, n_var))
+        self.objective = np.zeros(batch)
+        self.status = np.zeros(batch, dtype=np.int32)
+        self.iterations = np.zeros(batch, dtype=np.int32)
+        self.n_factor = np.zeros(batch, dtype=np.int32)
+        self.nlp_error = np.zeros(batch)
+
+    def struct(self):
+        r = ObcaResult()
+        for name in ("x", "objective", "status", "iterations", "n_factor", "nlp_error"):
+            setattr(r, name, getattr(self, name).ctypes.data)
+        return r
+
+
+class Context:
+    """Owns one htp_ctx (device workspace)."""
+
+    def __init__(self, device=0, options=None, lib=None):
+        self.lib = lib or load()
+        self.ctx = self.lib.htp_create(int(device))
+        if not self.ctx:
+            raise RuntimeError("[htp] htp_create failed")
+        for k, v in (options or {}).items():
+            self.set_option(k, v)
+
+    def set_option(self, name, value):
+        if self.lib.htp_set_option(self.ctx, name.encode(), float(value)) != 0:
+            raise ValueError(f"[htp] unknown option {name}")
+
+    def error(self):
+        return self.lib.htp_last_error(self.ctx).decode()
+
+    def solve(self, packed):
+        res = HostResults(packed.batch, packed.n_var)
+        b, r = packed.struct(), res.struct()
+        rc = self.lib.htp_obca_solve_batch(self.ctx, ctypes.byref(b), ctypes.byref(r))
+        if rc != 0:
+            raise RuntimeError(f"[htp] htp_obca_solve_batch failed: {self.error()}")
+        return res
+
+    def solve_device(self, packed, dev_ptrs, out_ptrs, stream=None):
+        b = packed.struct(dev_ptrs)
+        r = ObcaResult()
+        for k, v in out_ptrs.items():
+            setattr(r, k, v)
+        rc = self.lib.htp_obca_solve_batch_device(self.ctx, ctypes.byref(b), ctypes.byref(r), stream)
+        if rc != 0:
+            raise RuntimeError(f"[htp] htp_obca_solve_batch_device failed: {self.error()}")
+
+    def last_kernel_ms(self):
+        return self.lib.htp_last_kernel_ms(self.ctx)
+
+    def close(self):
+        if self.ctx:
+            self.lib.htp_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

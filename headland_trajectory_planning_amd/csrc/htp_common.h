@@ -1,0 +1,131 @@
+// Shared definitions for the batched OBCA interior-point solver.
+//
+// Problem layout follows R/obca_py/optimizer.py exactly (variables :292-354,
+// constraints :356-425, objective :427-473); the algorithm is the IPOPT
+// restatement documented in oracle/ipm.py (and DESIGN.md section 3).
+#pragma once
+#include <cstdint>
+
+#ifndef HTP_HD
+#error "define HTP_HD (__host__ __device__ or empty) before including htp_common.h"
+#endif
+
+namespace htp {
+
+constexpr int NS = 5;       // state  [x, y, v, theta, steer]
+constexpr int NC = 2;       // control [accel, steer_rate]
+constexpr int MAXM = 16;    // obstacles per problem
+constexpr int MAXK = 4;     // vehicle bodies per problem
+constexpr int MAXE = 8;     // edges per polytope
+constexpr int NBMAX = 13;   // stage block: 5 multipliers + 5 x + 2 u + 1 tau
+
+// per-problem scalar parameters (host packs them; see include/htp.h)
+enum Param {
+  P_DT = 0, P_Q00, P_Q01, P_Q10, P_Q11, P_R00, P_R01, P_R10, P_R11, P_W00, P_W11,
+  P_WHEELBASE, P_MAXSTEER, P_MAXV, P_MAXACC, P_MAXSR, P_DMIN, P_XLO, P_XHI, P_YLO, P_YHI,
+  P_HAS_INIT_CONTROL, P_HAS_INIT_DUAL, NPARAM = 24
+};
+
+// IPOPT option values (defaults in oracle/ipm.py OPTS)
+struct Options {
+  double tol, dual_inf_tol, constr_viol_tol, compl_inf_tol;
+  double acceptable_tol, acceptable_constr_viol_tol, acceptable_compl_inf_tol, acceptable_dual_inf_tol;
+  int acceptable_iter, max_iter, max_soc, pad0;
+  double bound_relax_factor, scaling_max_gradient, scaling_min_value;
+  double bound_push, bound_frac, bound_mult_init_val, constr_mult_init_max;
+  double mu_init, kappa_eps, kappa_mu, theta_mu, tau_min, kappa_sigma, kappa_d, s_max;
+  double gamma_theta, gamma_phi, delta, s_theta, s_phi, eta_phi, alpha_min_frac, kappa_soc;
+  double dw0, dw_min, dw_max, kw_minus, kw_plus, kw_plus_bar, dc_bar, kappa_c;
+};
+
+inline Options default_options() {
+  Options o{};
+  o.tol = 1e-8; o.dual_inf_tol = 1.0; o.constr_viol_tol = 1e-4; o.compl_inf_tol = 1e-4;
+  o.acceptable_tol = 1e-6; o.acceptable_constr_viol_tol = 1e-2; o.acceptable_compl_inf_tol = 1e-2;
+  o.acceptable_dual_inf_tol = 1e10; o.acceptable_iter = 15; o.max_iter = 3000; o.max_soc = 4;
+  o.bound_relax_factor = 1e-8; o.scaling_max_gradient = 100.0; o.scaling_min_value = 1e-8;
+  o.bound_push = 1e-2; o.bound_frac = 1e-2; o.bound_mult_init_val = 1.0; o.constr_mult_init_max = 1e3;
+  o.mu_init = 0.1; o.kappa_eps = 10.0; o.kappa_mu = 0.2; o.theta_mu = 1.5; o.tau_min = 0.99;
+  o.kappa_sigma = 1e10; o.kappa_d = 1e-5; o.s_max = 100.0;
+  o.gamma_theta = 1e-5; o.gamma_phi = 1e-8; o.delta = 1.0; o.s_theta = 1.1; o.s_phi = 2.3;
+  o.eta_phi = 1e-8; o.alpha_min_frac = 0.05; o.kappa_soc = 0.99;
+  o.dw0 = 1e-4; o.dw_min = 1e-20; o.dw_max = 1e40; o.kw_minus = 1.0 / 3.0; o.kw_plus = 8.0;
+  o.kw_plus_bar = 100.0; o.dc_bar = 1e-8; o.kappa_c = 0.25;
+  return o;
+}
+
+// Batch-uniform problem shape (all problems of one launch share it).
+struct Dims {
+  int N, M, K, topt;
+  int eo[MAXM], eb[MAXK], offo[MAXM], offb[MAXK];
+  int TEo, TEb, mu_count, lam_count, P;
+  int n, mc, md;               // variables, equality rows, inequality rows
+  int oU, oMU, oLAM, oTAU, oS; // variable offsets (optimizer.py:292-354)
+  int eDyn, eTerm, ePair;      // equality-row offsets
+  int nb, nw;                  // stage block size (12 + topt), stage w size (7 + topt)
+};
+
+// Offsets (in doubles) of the per-problem workspace arrays.
+struct Layout {
+  int64_t x, xL, xU, zL, zU, gf, dx, xt, rx, sx, dzL, dzU;   // n
+  int64_t s, dL, dU, vL, vU, d, ds, st, dt, yd, scI, dyd, rs, rd, dsoc, ss, syd, dvL, dvU;  // md
+  int64_t yc, c, scE, dyc, rc, ct, csoc, syc;                 // mc
+  int64_t pairS, pairR;                                      // 6P, 3P
+  int64_t Kst, Off, LD, fac, V, X;                           // stage storage
+  int64_t ipiv;                                              // ints stored as double
+  int64_t total;
+};
+
+struct Result {            // per problem
+  int32_t status, iters, n_factor, pad;
+  double objective, final_mu, nlp_error, sf;
+};
+
+enum Status { ST_SUCCESS = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_RESTORATION = 3, ST_STEPFAIL = 4,
+              ST_BADINPUT = 5 };
+
+HTP_HD inline void make_dims(Dims& d, int N, int M, int K, int topt, const int* eo, const int* eb) {
+  d.N = N; d.M = M; d.K = K; d.topt = topt ? 1 : 0;
+  d.TEo = 0; d.TEb = 0;
+  for (int m = 0; m < M; ++m) { d.eo[m] = eo[m]; d.offo[m] = d.TEo; d.TEo += eo[m]; }
+  for (int k = 0; k < K; ++k) { d.eb[k] = eb[k]; d.offb[k] = d.TEb; d.TEb += eb[k]; }
+  d.mu_count = d.TEb * M;
+  d.lam_count = d.TEo * K;
+  d.P = N * M * K;
+  d.oU = NS * N;
+  d.oMU = d.oU + NC * (N - 1);
+  d.oLAM = d.oMU + N * d.mu_count;
+  d.oTAU = d.oLAM + N * d.lam_count;
+  d.oS = d.oTAU + (d.topt ? N - 1 : 0);
+  d.n = d.oS + NS;
+  d.eDyn = NS;
+  d.eTerm = NS + NS * (N - 1);
+  d.ePair = d.eTerm + NS;
+  d.mc = d.ePair + 2 * d.P;
+  d.md = 2 * d.P;
+  d.nw = 7 + d.topt;
+  d.nb = NS + d.nw;
+}
+
+inline Layout make_layout(const Dims& d) {
+  Layout L{};
+  int64_t o = 0;
+  auto take = [&](int64_t cnt) { int64_t r = o; o += (cnt + 7) & ~int64_t(7); return r; };
+  L.x = take(d.n); L.xL = take(d.n); L.xU = take(d.n); L.zL = take(d.n); L.zU = take(d.n);
+  L.gf = take(d.n); L.dx = take(d.n); L.xt = take(d.n); L.rx = take(d.n); L.sx = take(d.n);
+  L.dzL = take(d.n); L.dzU = take(d.n);
+  L.s = take(d.md); L.dL = take(d.md); L.dU = take(d.md); L.vL = take(d.md); L.vU = take(d.md);
+  L.d = take(d.md); L.ds = take(d.md); L.st = take(d.md); L.dt = take(d.md); L.yd = take(d.md);
+  L.scI = take(d.md); L.dyd = take(d.md); L.rs = take(d.md); L.rd = take(d.md); L.dsoc = take(d.md);
+  L.ss = take(d.md); L.syd = take(d.md); L.dvL = take(d.md); L.dvU = take(d.md);
+  L.yc = take(d.mc); L.c = take(d.mc); L.scE = take(d.mc); L.dyc = take(d.mc); L.rc = take(d.mc);
+  L.ct = take(d.mc); L.csoc = take(d.mc); L.syc = take(d.mc);
+  L.pairS = take(6 * (int64_t)d.P); L.pairR = take(3 * (int64_t)d.P);
+  const int64_t nb2 = (int64_t)d.nb * d.nb;
+  L.Kst = take(d.N * nb2); L.Off = take(d.N * nb2); L.LD = take(d.N * nb2); L.fac = take(d.N * nb2);
+  L.V = take((int64_t)d.N * d.nb); L.X = take((int64_t)d.N * d.nb); L.ipiv = take((int64_t)d.N * d.nb);
+  L.total = o;
+  return L;
+}
+
+}  // namespace htp

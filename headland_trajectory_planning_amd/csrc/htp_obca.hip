@@ -1,0 +1,226 @@
+// libhtp.so: batched OBCA interior-point solver for gfx950 (MI355X) + C ABI.
+//
+// One 64-lane wavefront (one workgroup) per headland-turn problem; the whole
+// IPOPT-restated solve (oracle/ipm.py) runs inside one kernel launch, so
+// problems converge independently and the hardware dispatcher refills a CU as
+// soon as a wave retires (no host round trip per iteration).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#define HTP_HD __host__ __device__
+#include "wave_ctx.h"
+#include "obca_batch.h"
+
+using namespace htp;
+
+namespace {
+
+constexpr int LDS_D = 4 * NBMAX * NBMAX + 8;
+
+__global__ __launch_bounds__(64) void obca_solve_kernel(Dims D, Layout L, Options o, BatchView b,
+                                                        double* __restrict__ ws_all, int64_t ws_stride,
+                                                        Result* __restrict__ res, double* __restrict__ xout,
+                                                        int batch) {
+  __shared__ double lds[LDS_D];
+  __shared__ int ilds[2 * NBMAX];
+  const int p = blockIdx.x;
+  if (p >= batch) return;
+  DevWave c{(int)threadIdx.x, lds, ilds};
+  ProblemIn in = problem_view(b, D, p);
+  double* ws = ws_all + (int64_t)p * ws_stride;
+  ObcaSolver<DevWave> S(c, D, L, o, in, ws);
+  Result r{};
+  S.run(r);
+  if (threadIdx.x == 0) res[p] = r;
+  const double* x = ws + L.x;
+  for (int q = threadIdx.x; q < D.n; q += 64) xout[(int64_t)p * D.n + q] = x[q];
+}
+
+__global__ void unpack_results(const Result* __restrict__ r, int batch, double* obj, int32_t* st, int32_t* it,
+                               int32_t* nf, double* err) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= batch) return;
+  if (obj) obj[p] = r[p].objective;
+  if (st) st[p] = r[p].status;
+  if (it) it[p] = r[p].iters;
+  if (nf) nf[p] = r[p].n_factor;
+  if (err) err[p] = r[p].nlp_error;
+}
+
+}  // namespace
+
+struct htp_ctx {
+  int device = 0;
+  std::string err;
+  Options opt = default_options();
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  void* scratch = nullptr;  // Result array
+  size_t scratch_bytes = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double last_ms = 0.0;
+};
+
+static int fail(htp_ctx* c, const std::string& m) {
+  if (c) c->err = m;
+  return -1;
+}
+
+#define HIPCHK(expr)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess) return fail(ctx, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+static int ensure(htp_ctx* ctx, void** p, size_t* have, size_t need) {
+  if (*have >= need) return 0;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  HIPCHK(hipMalloc(p, need));
+  *have = need;
+  return 0;
+}
+
+extern "C" {
+
+int htp_obca_sizes(int32_t N, int32_t M, int32_t K, int32_t time_opt, const int32_t* eo, const int32_t* eb,
+                   int64_t* n_var, int64_t* n_eq, int64_t* n_ineq, int64_t* ws_doubles) {
+  if (N < 2 || M < 1 || M > MAXM || K < 1 || K > MAXK) return -1;
+  Dims D;
+  make_dims(D, N, M, K, time_opt, eo, eb);
+  Layout L = make_layout(D);
+  if (n_var) *n_var = D.n;
+  if (n_eq) *n_eq = D.mc;
+  if (n_ineq) *n_ineq = D.md;
+  if (ws_doubles) *ws_doubles = L.total;
+  return 0;
+}
+
+htp_ctx* htp_create(int32_t device) {
+  htp_ctx* c = new htp_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    c->err = "hipSetDevice failed";
+    return c;
+  }
+  (void)hipEventCreate(&c->ev0);
+  (void)hipEventCreate(&c->ev1);
+  return c;
+}
+
+void htp_destroy(htp_ctx* c) {
+  if (!c) return;
+  if (c->ws) (void)hipFree(c->ws);
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  delete c;
+}
+
+const char* htp_last_error(htp_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int htp_set_option(htp_ctx* ctx, const char* name, double v) {
+  if (!ctx || !name) return -1;
+  if (set_option(ctx->opt, name, v)) return fail(ctx, std::string("unknown option ") + name);
+  return 0;
+}
+
+double htp_last_kernel_ms(htp_ctx* c) { return c ? c->last_ms : 0.0; }
+
+int htp_obca_solve_batch_device(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result* out, void* stream) {
+  if (!ctx || !in || !out) return -1;
+  const char* e = nullptr;
+  if (check_shape(in, &e)) return fail(ctx, e);
+  if (in->batch == 0) return 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  Dims D;
+  make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
+  Layout L = make_layout(D);
+  const size_t need = (size_t)L.total * sizeof(double) * (size_t)in->batch;
+  if (ensure(ctx, &ctx->ws, &ctx->ws_bytes, need)) return -1;
+  if (ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, sizeof(Result) * (size_t)in->batch)) return -1;
+  BatchView b{in->traj, in->obs_A, in->obs_b, in->body_G, in->body_g, in->params,
+              in->init_control, in->init_mu, in->init_lambda};
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipEventRecord(ctx->ev0, s));
+  hipLaunchKernelGGL(obca_solve_kernel, dim3(in->batch), dim3(64), 0, s, D, L, ctx->opt, b, (double*)ctx->ws,
+                     (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ctx->ev1, s));
+  hipLaunchKernelGGL(unpack_results, dim3((in->batch + 255) / 256), dim3(256), 0, s, (const Result*)ctx->scratch,
+                     in->batch, out->objective, out->status, out->iterations, out->n_factor, out->nlp_error);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int htp_obca_solve_batch(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result* out) {
+  if (!ctx || !in || !out) return -1;
+  const char* e = nullptr;
+  if (check_shape(in, &e)) return fail(ctx, e);
+  if (in->batch == 0) return 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  Dims D;
+  make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
+  const int64_t B = in->batch;
+  auto bytes = [&](int64_t n) { return (size_t)(n * (int64_t)sizeof(double)); };
+  const size_t sz_traj = bytes(B * D.N * NS), sz_A = bytes(B * D.TEo * 2), sz_b = bytes(B * D.TEo);
+  const size_t sz_G = bytes(B * D.TEb * 2), sz_g = bytes(B * D.TEb), sz_p = bytes(B * NPARAM);
+  const size_t sz_u = in->init_control ? bytes(B * (D.N - 1) * NC) : 0;
+  const size_t sz_mu = in->init_mu ? bytes(B * D.N * D.mu_count) : 0;
+  const size_t sz_la = in->init_lambda ? bytes(B * D.N * D.lam_count) : 0;
+  const size_t sz_x = bytes(B * D.n);
+  std::vector<size_t> sizes = {sz_traj, sz_A, sz_b, sz_G, sz_g, sz_p, sz_u, sz_mu, sz_la, sz_x,
+                               bytes(B), (size_t)B * 4, (size_t)B * 4, (size_t)B * 4, bytes(B)};
+  size_t total = 0;
+  std::vector<size_t> off;
+  for (size_t s : sizes) { off.push_back(total); total += (s + 255) & ~size_t(255); }
+  char* dev = nullptr;
+  HIPCHK(hipMalloc((void**)&dev, total));
+  const void* srcs[9] = {in->traj, in->obs_A, in->obs_b, in->body_G, in->body_g, in->params,
+                         in->init_control, in->init_mu, in->init_lambda};
+  for (int k = 0; k < 9; ++k)
+    if (sizes[k]) {
+      hipError_t er = hipMemcpy(dev + off[k], srcs[k], sizes[k], hipMemcpyHostToDevice);
+      if (er != hipSuccess) { (void)hipFree(dev); return fail(ctx, hipGetErrorString(er)); }
+    }
+  htp_obca_batch din = *in;
+  din.traj = (const double*)(dev + off[0]);
+  din.obs_A = (const double*)(dev + off[1]);
+  din.obs_b = (const double*)(dev + off[2]);
+  din.body_G = (const double*)(dev + off[3]);
+  din.body_g = (const double*)(dev + off[4]);
+  din.params = (const double*)(dev + off[5]);
+  din.init_control = sz_u ? (const double*)(dev + off[6]) : nullptr;
+  din.init_mu = sz_mu ? (const double*)(dev + off[7]) : nullptr;
+  din.init_lambda = sz_la ? (const double*)(dev + off[8]) : nullptr;
+  htp_obca_result dout;
+  dout.x = (double*)(dev + off[9]);
+  dout.objective = (double*)(dev + off[10]);
+  dout.status = (int32_t*)(dev + off[11]);
+  dout.iterations = (int32_t*)(dev + off[12]);
+  dout.n_factor = (int32_t*)(dev + off[13]);
+  dout.nlp_error = (double*)(dev + off[14]);
+  int rc = htp_obca_solve_batch_device(ctx, &din, &dout, nullptr);
+  if (rc == 0) {
+    hipError_t er = hipDeviceSynchronize();
+    if (er != hipSuccess) rc = fail(ctx, std::string("solve kernel: ") + hipGetErrorString(er));
+  }
+  if (rc == 0) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) == hipSuccess) ctx->last_ms = ms;
+    struct { void* dst; size_t off, sz; } outs[6] = {{out->x, off[9], sz_x}, {out->objective, off[10], bytes(B)},
+                                                     {out->status, off[11], (size_t)B * 4}, {out->iterations, off[12], (size_t)B * 4},
+                                                     {out->n_factor, off[13], (size_t)B * 4}, {out->nlp_error, off[14], bytes(B)}};
+    for (auto& o : outs)
+      if (o.dst && hipMemcpy(o.dst, dev + o.off, o.sz, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(ctx, "copy back");
+  }
+  (void)hipFree(dev);
+  return rc;
+}
+
+}  // extern "C"

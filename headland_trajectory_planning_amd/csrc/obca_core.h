@@ -1,0 +1,1717 @@
+// Batched OBCA interior-point solver core: one problem per wavefront.
+//
+// NLP: R/obca_py/optimizer.py (variables :292-354, constraints :356-425,
+// objective :427-473, dynamics :9-36 / :364-377).  Algorithm: the IPOPT 3.14
+// default path restated in oracle/ipm.py (that file lists every constant).
+// Linear algebra: structure-exploiting Schur eliminations of DESIGN.md s.3
+// (same order as oracle/structured.py):
+//   inequality slacks/multipliers -> per-(stage,obstacle,body) local blocks
+//   -> terminal slack block -> block-tridiagonal stage LDL^T (Bunch-Kaufman
+//   per 13x13 block), giving the exact inertia by Sylvester's law.
+//
+// Parallel model: every "for (q = c.lane; q < n; q += c.width)" loop is a
+// lane-parallel sweep with independent iterations; c.sync() separates
+// sweeps; c.sum()/maxv() are wave reductions.  All control flow outside the
+// sweeps is wave-uniform.
+#pragma once
+#include <cmath>
+
+#include "htp_common.h"
+#include "dyn_gen.h"
+
+namespace htp {
+
+struct ProblemIn {
+  const double* traj;    // N x 5
+  const double* obsA;    // TEo x 2
+  const double* obsb;    // TEo
+  const double* bodyG;   // TEb x 2
+  const double* bodyg;   // TEb
+  const double* par;     // NPARAM
+  const double* init_u;  // (N-1) x 2 or null
+  const double* init_mu; // N x mu_count or null
+  const double* init_la; // N x lam_count or null
+};
+
+HTP_HD inline double sq(double a) { return a * a; }
+HTP_HD inline bool finite_(double a) { return a > -1e300 && a < 1e300; }
+HTP_HD inline double dmax(double a, double b) { return a > b ? a : b; }
+HTP_HD inline double dmin(double a, double b) { return a < b ? a : b; }
+HTP_HD inline double dabs(double a) { return a < 0 ? -a : a; }
+
+constexpr double HTP_INF = __builtin_huge_val();
+
+// ---------------------------------------------------------------------------
+// Local (stage, obstacle m, body n) block:  z = [mu_mn (EN), lam_mn (EM)],
+// rows c2a, c2b (equality), coupled to p = (x_i, y_i, theta_i).
+// Inequality rows c1 (||A'lam||^2 in [0,1]) and c3 (distance >= dmin) are
+// already eliminated (Hbar = W + Sigma + dw + Jd' E^-1 Jd).
+// ---------------------------------------------------------------------------
+template <int EN, int EM>
+struct LocalBlock {
+  static constexpr int NZ = EN + EM;
+  static constexpr int NL = NZ + 2;
+  static constexpr int NPK = NL * (NL + 1) / 2;
+  double K[NPK];       // packed lower; becomes L (unit, strict lower) + D (diag)
+  double B[NL][3];     // coupling to p = (x, y, theta)
+  double Hpp[6];       // direct p-p terms: xx xy yy xt yt tt
+  double J1[NZ], J3z[NZ], J3p[2];
+  double E1, E3, Ds1, Ds3;
+  int neg, zero;
+
+  HTP_HD static int pk(int r, int c) { return r * (r + 1) / 2 + c; }
+
+  HTP_HD void factor() {  // unpivoted LDL^T of K (inertia = signs of D)
+    neg = 0;
+    zero = 0;
+    for (int k = 0; k < NL; ++k) {
+      double dk = K[pk(k, k)];
+      for (int j = 0; j < k; ++j) dk -= K[pk(k, j)] * K[pk(k, j)] * K[pk(j, j)];
+      if (dk == 0.0) { zero = 1; dk = 1.0; }
+      if (dk < 0.0) ++neg;
+      K[pk(k, k)] = dk;
+      for (int r = k + 1; r < NL; ++r) {
+        double v = K[pk(r, k)];
+        for (int j = 0; j < k; ++j) v -= K[pk(r, j)] * K[pk(k, j)] * K[pk(j, j)];
+        K[pk(r, k)] = v / dk;
+      }
+    }
+  }
+  HTP_HD void solve(double* v) const {  // in place K^-1 v
+    for (int k = 0; k < NL; ++k)
+      for (int j = 0; j < k; ++j) v[k] -= K[pk(k, j)] * v[j];
+    for (int k = 0; k < NL; ++k) v[k] /= K[pk(k, k)];
+    for (int k = NL - 1; k >= 0; --k)
+      for (int r = k + 1; r < NL; ++r) v[k] -= K[pk(r, k)] * v[r];
+  }
+};
+
+// ---------------------------------------------------------------------------
+template <class Ctx>
+struct ObcaSolver {
+  Ctx& c;
+  const Dims& D;
+  const Layout& L;
+  const Options& o;
+  const ProblemIn& in;
+  double* ws;
+
+  // scalar state (wave-uniform)
+  double sf, mu, tau, dw_last;
+  double theta_min, theta_max;
+  int n_factor;
+  // filter (wave-uniform, small)
+  static constexpr int FMAX = 64;
+  double f_th[FMAX], f_ph[FMAX];
+  int nfilt;
+
+  HTP_HD ObcaSolver(Ctx& c_, const Dims& D_, const Layout& L_, const Options& o_, const ProblemIn& in_, double* ws_)
+      : c(c_), D(D_), L(L_), o(o_), in(in_), ws(ws_) {}
+
+  HTP_HD double* A(int64_t off) const { return ws + off; }
+  HTP_HD double par(int k) const { return in.par[k]; }
+  HTP_HD double tauv(const double* x, int i) const { return D.topt ? x[D.oTAU + i] : 1.0; }
+
+  // pair p -> (i, m, n) and variable offsets
+  HTP_HD void pair_index(int p, int& i, int& m, int& n, int& mu0, int& la0) const {
+    n = p % D.K;
+    int t = p / D.K;
+    m = t % D.M;
+    i = t / D.M;
+    mu0 = D.oMU + i * D.mu_count + m * D.TEb + D.offb[n];
+    la0 = D.oLAM + i * D.lam_count + n * D.TEo + D.offo[m];
+  }
+
+  // stage w = [x_i (5), u_i (2), tau_i]
+  HTP_HD void stage_w(const double* x, int i, double* w) const {
+    for (int k = 0; k < NS; ++k) w[k] = x[NS * i + k];
+    w[5] = x[D.oU + NC * i];
+    w[6] = x[D.oU + NC * i + 1];
+    if (D.topt) w[7] = x[D.oTAU + i];
+  }
+  HTP_HD void dynF(const double* w, double* F) const {
+    if (D.topt) dyn_F_rk2(w, par(P_DT), par(P_WHEELBASE), F);
+    else dyn_F_euler(w, par(P_DT), par(P_WHEELBASE), F);
+  }
+  HTP_HD void dynJ(const double* w, double* J) const {
+    if (D.topt) dyn_J_rk2(w, par(P_DT), par(P_WHEELBASE), J);
+    else dyn_J_euler(w, par(P_DT), par(P_WHEELBASE), J);
+  }
+  HTP_HD void dynH(const double* w, const double* y, double* H) const {
+    if (D.topt) dyn_H_rk2(w, par(P_DT), par(P_WHEELBASE), y, H);
+    else dyn_H_euler(w, par(P_DT), par(P_WHEELBASE), y, H);
+  }
+
+  // ======================================================== objective
+  // f (unscaled) -- optimizer.py:447-473
+  HTP_HD double stage_obj(const double* x, int i) const {
+    const int N = D.N;
+    const double dT = par(P_DT);
+    double f = 0.0;
+    if (i < N - 1) {
+      const double h = dT * tauv(x, i);
+      const double a = x[D.oU + NC * i], w = x[D.oU + NC * i + 1];
+      if (D.topt) f += h * par(P_W11);
+      f += a * (par(P_Q00) * a + par(P_Q01) * w) + w * (par(P_Q10) * a + par(P_Q11) * w);
+      if (i < N - 2) {
+        const double ja = (x[D.oU + NC * (i + 1)] - a) / h, jw = (x[D.oU + NC * (i + 1) + 1] - w) / h;
+        f += ja * (par(P_R00) * ja + par(P_R01) * jw) + jw * (par(P_R10) * ja + par(P_R11) * jw);
+      }
+      f += sq(x[NS * i + 2] * h) * par(P_W00);
+    }
+    if (i == 0)
+      for (int k = 0; k < NS; ++k) f += 5000.0 * sq(x[D.oS + k]);
+    return f;
+  }
+  HTP_HD double eval_f(const double* x) const {
+    double f = 0.0;
+    for (int i = c.lane; i < D.N; i += c.width) f += stage_obj(x, i);
+    return c.sum(f);
+  }
+  // scaled gradient (sf * grad f) into g (all n entries written)
+  HTP_HD void eval_grad_f(const double* x, double* g, double scale) const {
+    const int N = D.N;
+    const double dT = par(P_DT);
+    const double Qs00 = 2 * par(P_Q00), Qs01 = par(P_Q01) + par(P_Q10), Qs11 = 2 * par(P_Q11);
+    const double Rs00 = 2 * par(P_R00), Rs01 = par(P_R01) + par(P_R10), Rs11 = 2 * par(P_R11);
+    for (int q = c.lane; q < D.n; q += c.width) g[q] = 0.0;
+    c.sync();
+    for (int i = c.lane; i < N - 1; i += c.width) {
+      const double tau = tauv(x, i), h = dT * tau;
+      const double a = x[D.oU + NC * i], w = x[D.oU + NC * i + 1];
+      double ga = Qs00 * a + Qs01 * w, gw = Qs01 * a + Qs11 * w;
+      double gt = D.topt ? dT * par(P_W11) : 0.0;
+      if (i < N - 2) {
+        const double da = x[D.oU + NC * (i + 1)] - a, dw_ = x[D.oU + NC * (i + 1) + 1] - w;
+        ga -= (Rs00 * da + Rs01 * dw_) / (h * h);
+        gw -= (Rs01 * da + Rs11 * dw_) / (h * h);
+        const double Jv = (da * (par(P_R00) * da + par(P_R01) * dw_) + dw_ * (par(P_R10) * da + par(P_R11) * dw_)) / (h * h);
+        gt += -2.0 * Jv / tau;
+      }
+      if (i >= 1) {
+        const double hp = dT * tauv(x, i - 1);
+        const double da = a - x[D.oU + NC * (i - 1)], dw_ = w - x[D.oU + NC * (i - 1) + 1];
+        ga += (Rs00 * da + Rs01 * dw_) / (hp * hp);
+        gw += (Rs01 * da + Rs11 * dw_) / (hp * hp);
+      }
+      const double v = x[NS * i + 2];
+      g[NS * i + 2] = scale * 2.0 * par(P_W00) * v * h * h;
+      if (D.topt) gt += 2.0 * par(P_W00) * v * v * dT * dT * tau;
+      g[D.oU + NC * i] = scale * ga;
+      g[D.oU + NC * i + 1] = scale * gw;
+      if (D.topt) g[D.oTAU + i] = scale * gt;
+    }
+    if (c.lane == 0)
+      for (int k = 0; k < NS; ++k) g[D.oS + k] = scale * 10000.0 * x[D.oS + k];
+    c.sync();
+  }
+
+  // ======================================================== constraints
+  // scaled c (equality) and d (inequality) at x (optimizer.py:356-425)
+  HTP_HD void pair_geom(const double* x, int p, double* w, double& cs, double& sn,
+                        int& i, int& m, int& n, int& mu0, int& la0) const {
+    pair_index(p, i, m, n, mu0, la0);
+    const int em = D.eo[m];
+    const double* Am = in.obsA + 2 * D.offo[m];
+    w[0] = w[1] = 0.0;
+    for (int j = 0; j < em; ++j) {
+      w[0] += Am[2 * j] * x[la0 + j];
+      w[1] += Am[2 * j + 1] * x[la0 + j];
+    }
+    const double th = x[NS * i + 3];
+    cs = cos(th);
+    sn = sin(th);
+  }
+
+  HTP_HD void pair_cons(const double* x, int p, double* out4) const {
+    double w[2], cs, sn;
+    int i, m, n, mu0, la0;
+    pair_geom(x, p, w, cs, sn, i, m, n, mu0, la0);
+    const int em = D.eo[m], en = D.eb[n];
+    const double* Am = in.obsA + 2 * D.offo[m];
+    const double* bm = in.obsb + D.offo[m];
+    const double* Gn = in.bodyG + 2 * D.offb[n];
+    const double* gn = in.bodyg + D.offb[n];
+    double c2a = cs * w[0] + sn * w[1], c2b = -sn * w[0] + cs * w[1], c3 = 0.0;
+    for (int j = 0; j < en; ++j) {
+      const double mu = x[mu0 + j];
+      c2a += Gn[2 * j] * mu;
+      c2b += Gn[2 * j + 1] * mu;
+      c3 -= gn[j] * mu;
+    }
+    const double tx = x[NS * i], ty = x[NS * i + 1];
+    for (int j = 0; j < em; ++j) c3 += (Am[2 * j] * tx + Am[2 * j + 1] * ty - bm[j]) * x[la0 + j];
+    out4[0] = w[0] * w[0] + w[1] * w[1];
+    out4[1] = c2a;
+    out4[2] = c2b;
+    out4[3] = c3;
+  }
+
+  HTP_HD void eval_cons(const double* x, double* cc, double* dd) const {
+    const int N = D.N;
+    const double* scE = A(L.scE);
+    const double* scI = A(L.scI);
+    for (int i = c.lane; i < N; i += c.width) {
+      if (i == 0)
+        for (int k = 0; k < NS; ++k) cc[k] = scE[k] * (x[k] - in.traj[k]);
+      if (i < N - 1) {
+        double w[8], F[5];
+        stage_w(x, i, w);
+        dynF(w, F);
+        for (int k = 0; k < NS; ++k) {
+          const int r = D.eDyn + NS * i + k;
+          cc[r] = scE[r] * (x[NS * (i + 1) + k] - F[k]);
+        }
+      } else {
+        for (int k = 0; k < NS; ++k) {
+          const int r = D.eTerm + k;
+          cc[r] = scE[r] * (x[NS * i + k] - in.traj[NS * i + k] + x[D.oS + k]);
+        }
+      }
+    }
+    for (int p = c.lane; p < D.P; p += c.width) {
+      double v[4];
+      pair_cons(x, p, v);
+      const int re = D.ePair + 2 * p;
+      cc[re] = scE[re] * v[1];
+      cc[re + 1] = scE[re + 1] * v[2];
+      dd[2 * p] = scI[2 * p] * v[0];
+      dd[2 * p + 1] = scI[2 * p + 1] * v[3];
+    }
+    c.sync();
+  }
+
+  // J_c' yc + J_d' yd (x part) into out (scaled rows; yc, yd multipliers of scaled rows)
+  HTP_HD void eval_jt(const double* x, const double* yc, const double* yd, double* out) {
+    const int N = D.N;
+    const double* scE = A(L.scE);
+    const double* scI = A(L.scI);
+    double* pr = A(L.pairR);
+    for (int q = c.lane; q < D.n; q += c.width) out[q] = 0.0;
+    c.sync();
+    for (int p = c.lane; p < D.P; p += c.width) {
+      double w[2], cs, sn;
+      int i, m, n, mu0, la0;
+      pair_geom(x, p, w, cs, sn, i, m, n, mu0, la0);
+      const int em = D.eo[m], en = D.eb[n];
+      const double* Am = in.obsA + 2 * D.offo[m];
+      const double* bm = in.obsb + D.offo[m];
+      const double* Gn = in.bodyG + 2 * D.offb[n];
+      const double* gn = in.bodyg + D.offb[n];
+      const int re = D.ePair + 2 * p;
+      const double ya = scE[re] * yc[re], yb = scE[re + 1] * yc[re + 1];
+      const double y1 = scI[2 * p] * yd[2 * p], y3 = scI[2 * p + 1] * yd[2 * p + 1];
+      for (int j = 0; j < en; ++j) out[mu0 + j] = Gn[2 * j] * ya + Gn[2 * j + 1] * yb - gn[j] * y3;
+      const double tx = x[NS * i], ty = x[NS * i + 1];
+      for (int j = 0; j < em; ++j) {
+        const double a0 = Am[2 * j], a1 = Am[2 * j + 1];
+        out[la0 + j] = (cs * a0 + sn * a1) * ya + (-sn * a0 + cs * a1) * yb + 2.0 * (a0 * w[0] + a1 * w[1]) * y1 +
+                       (a0 * tx + a1 * ty - bm[j]) * y3;
+      }
+      pr[3 * p + 0] = w[0] * y3;
+      pr[3 * p + 1] = w[1] * y3;
+      pr[3 * p + 2] = (-sn * w[0] + cs * w[1]) * ya + (-cs * w[0] - sn * w[1]) * yb;
+    }
+    c.sync();
+    const int MK = D.M * D.K;
+    for (int i = c.lane; i < N; i += c.width) {
+      double gx[5] = {0, 0, 0, 0, 0};
+      if (i == 0)
+        for (int k = 0; k < NS; ++k) gx[k] += scE[k] * yc[k];
+      else
+        for (int k = 0; k < NS; ++k) gx[k] += scE[D.eDyn + NS * (i - 1) + k] * yc[D.eDyn + NS * (i - 1) + k];
+      if (i == N - 1) {
+        for (int k = 0; k < NS; ++k) {
+          const double t = scE[D.eTerm + k] * yc[D.eTerm + k];
+          gx[k] += t;
+          out[D.oS + k] = t;
+        }
+      } else {
+        double w[8], J[40], yy[5];
+        stage_w(x, i, w);
+        dynJ(w, J);
+        for (int k = 0; k < NS; ++k) yy[k] = scE[D.eDyn + NS * i + k] * yc[D.eDyn + NS * i + k];
+        double gw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < NS; ++k)
+          for (int j = 0; j < D.nw; ++j) gw[j] -= J[k * D.nw + j] * yy[k];
+        for (int k = 0; k < NS; ++k) gx[k] += gw[k];
+        out[D.oU + NC * i] = gw[5];
+        out[D.oU + NC * i + 1] = gw[6];
+        if (D.topt) out[D.oTAU + i] = gw[7];
+      }
+      for (int q = 0; q < MK; ++q) {
+        const int p = i * MK + q;
+        gx[0] += pr[3 * p];
+        gx[1] += pr[3 * p + 1];
+        gx[3] += pr[3 * p + 2];
+      }
+      for (int k = 0; k < NS; ++k) out[NS * i + k] = gx[k];
+    }
+    c.sync();
+  }
+
+  // ======================================================== setup
+  HTP_HD void set_bounds_and_x0() {
+    const int N = D.N;
+    double* x = A(L.x);
+    double* xL = A(L.xL);
+    double* xU = A(L.xU);
+    const double vmax = dabs(par(P_MAXV)), smax = dabs(par(P_MAXSTEER));
+    const double amax = dabs(par(P_MAXACC)), wmax = dabs(par(P_MAXSR));
+    const double twopi = 2.0 * M_PI;
+    for (int q = c.lane; q < D.n; q += c.width) {
+      double lo = -HTP_INF, hi = HTP_INF, v0 = 0.0;
+      if (q < D.oU) {
+        const int i = q / NS, k = q % NS;
+        v0 = in.traj[q];
+        if (k == 0) { lo = par(P_XLO); hi = par(P_XHI); }
+        if (k == 1) { lo = par(P_YLO); hi = par(P_YHI); }
+        if (k == 2) { lo = -vmax; hi = vmax; }
+        if (k == 3) { lo = -twopi; hi = twopi; }
+        if (k == 4) { lo = -smax; hi = smax; }
+        (void)i;
+      } else if (q < D.oMU) {
+        const int j = q - D.oU;
+        v0 = in.init_u ? in.init_u[j] : 0.0;
+        if (j % 2 == 0) { lo = -amax; hi = amax; } else { lo = -wmax; hi = wmax; }
+      } else if (q < D.oLAM) {
+        v0 = in.init_mu ? in.init_mu[q - D.oMU] : 0.1;
+        lo = 0.0;
+      } else if (q < D.oTAU) {
+        v0 = in.init_la ? in.init_la[q - D.oLAM] : 0.1;
+        lo = 0.0;
+      } else if (q < D.oS) {
+        v0 = 1.0;
+        lo = 0.05 / par(P_DT);
+        hi = 1.0;
+      }
+      x[q] = v0;
+      xL[q] = lo;
+      xU[q] = hi;
+    }
+    c.sync();
+  }
+
+  // gradient-based scaling at the user x0 (IPOPT nlp_scaling_method default)
+  HTP_HD void compute_scaling() {
+    const int N = D.N;
+    const double* x = A(L.x);
+    double* g = A(L.gf);
+    eval_grad_f(x, g, 1.0);
+    double mg = 0.0;
+    for (int q = c.lane; q < D.n; q += c.width) mg = dmax(mg, dabs(g[q]));
+    mg = c.maxv(mg);
+    sf = mg > o.scaling_max_gradient ? dmax(o.scaling_min_value, o.scaling_max_gradient / mg) : 1.0;
+    double* scE = A(L.scE);
+    double* scI = A(L.scI);
+    auto scl = [&](double rm) {
+      return rm > o.scaling_max_gradient ? dmax(o.scaling_min_value, o.scaling_max_gradient / rm) : 1.0;
+    };
+    for (int i = c.lane; i < N; i += c.width) {
+      if (i == 0)
+        for (int k = 0; k < NS; ++k) scE[k] = 1.0;
+      if (i < N - 1) {
+        double w[8], J[40];
+        stage_w(x, i, w);
+        dynJ(w, J);
+        for (int k = 0; k < NS; ++k) {
+          double rm = 1.0;  // +1 at x_{i+1,k}
+          for (int j = 0; j < D.nw; ++j) rm = dmax(rm, dabs(J[k * D.nw + j]));
+          scE[D.eDyn + NS * i + k] = scl(rm);
+        }
+      } else {
+        for (int k = 0; k < NS; ++k) scE[D.eTerm + k] = 1.0;
+      }
+    }
+    for (int p = c.lane; p < D.P; p += c.width) {
+      double w[2], cs, sn;
+      int i, m, n, mu0, la0;
+      pair_geom(x, p, w, cs, sn, i, m, n, mu0, la0);
+      const int em = D.eo[m], en = D.eb[n];
+      const double* Am = in.obsA + 2 * D.offo[m];
+      const double* bm = in.obsb + D.offo[m];
+      const double* Gn = in.bodyG + 2 * D.offb[n];
+      const double* gn = in.bodyg + D.offb[n];
+      double r1 = 0, ra = 0, rb = 0, r3 = 0;
+      const double tx = x[NS * i], ty = x[NS * i + 1];
+      for (int j = 0; j < em; ++j) {
+        const double a0 = Am[2 * j], a1 = Am[2 * j + 1];
+        r1 = dmax(r1, dabs(2.0 * (a0 * w[0] + a1 * w[1])));
+        ra = dmax(ra, dabs(cs * a0 + sn * a1));
+        rb = dmax(rb, dabs(-sn * a0 + cs * a1));
+        r3 = dmax(r3, dabs(a0 * tx + a1 * ty - bm[j]));
+      }
+      for (int j = 0; j < en; ++j) {
+        ra = dmax(ra, dabs(Gn[2 * j]));
+        rb = dmax(rb, dabs(Gn[2 * j + 1]));
+        r3 = dmax(r3, dabs(gn[j]));
+      }
+      ra = dmax(ra, dabs(-sn * w[0] + cs * w[1]));
+      rb = dmax(rb, dabs(-cs * w[0] - sn * w[1]));
+      r3 = dmax(r3, dmax(dabs(w[0]), dabs(w[1])));
+      scE[D.ePair + 2 * p] = scl(ra);
+      scE[D.ePair + 2 * p + 1] = scl(rb);
+      scI[2 * p] = scl(r1);
+      scI[2 * p + 1] = scl(r3);
+    }
+    c.sync();
+  }
+
+  HTP_HD void relax_and_push() {
+    double* x = A(L.x);
+    double* xL = A(L.xL);
+    double* xU = A(L.xU);
+    const double rf = o.bound_relax_factor;
+    for (int q = c.lane; q < D.n; q += c.width) {
+      double lo = xL[q], hi = xU[q];
+      const bool hl = finite_(lo), hu = finite_(hi);
+      if (hl) lo -= rf * dmax(1.0, dabs(lo));
+      if (hu) hi += rf * dmax(1.0, dabs(hi));
+      xL[q] = lo;
+      xU[q] = hi;
+      x[q] = push(x[q], lo, hi, hl, hu);
+    }
+    c.sync();
+  }
+
+  HTP_HD double push(double v, double lo, double hi, bool hl, bool hu) const {
+    double pl = hl ? o.bound_push * dmax(1.0, dabs(lo)) : 0.0;
+    double pu = hu ? o.bound_push * dmax(1.0, dabs(hi)) : 0.0;
+    if (hl && hu) {
+      pl = dmin(pl, o.bound_frac * (hi - lo));
+      pu = dmin(pu, o.bound_frac * (hi - lo));
+    }
+    if (hl) v = dmax(v, lo + pl);
+    if (hu) v = dmin(v, hi - pu);
+    return v;
+  }
+
+  // inequality-row bounds: c1 in [0,1], c3 in [dmin, inf), relaxed and scaled
+  HTP_HD void set_slack_bounds_and_push() {
+    const double rf = o.bound_relax_factor;
+    double dmn = par(P_DMIN);
+    double* s = A(L.s);
+    double* dL = A(L.dL);
+    double* dU = A(L.dU);
+    const double* d = A(L.d);
+    const double* scI = A(L.scI);
+    for (int r = c.lane; r < D.md; r += c.width) {
+      double lo, hi;
+      if ((r & 1) == 0) { lo = 0.0; hi = 1.0; } else { lo = dmn; hi = HTP_INF; }
+      const bool hl = true, hu = finite_(hi);
+      lo -= rf * dmax(1.0, dabs(lo));
+      if (hu) hi += rf * dmax(1.0, dabs(hi));
+      lo *= scI[r];
+      if (hu) hi *= scI[r];
+      dL[r] = lo;
+      dU[r] = hi;
+      s[r] = push(d[r], lo, hi, hl, hu);
+    }
+    c.sync();
+  }
+
+  // ======================================================== KKT assembly
+  // mode_ls: least-squares multiplier system (W=0, identity x/s blocks)
+  template <int EN, int EM>
+  HTP_HD void build_local(LocalBlock<EN, EM>& B, int p, bool ls, double dw, double dc) const {
+    const double* x = A(L.x);
+    double w[2], cs, sn;
+    int i, m, n, mu0, la0;
+    pair_geom(x, p, w, cs, sn, i, m, n, mu0, la0);
+    const int em = D.eo[m], en = D.eb[n];
+    const double* Am = in.obsA + 2 * D.offo[m];
+    const double* bm = in.obsb + D.offo[m];
+    const double* Gn = in.bodyG + 2 * D.offb[n];
+    const double* gn = in.bodyg + D.offb[n];
+    const double* scE = A(L.scE);
+    const double* scI = A(L.scI);
+    const double* yc = A(L.yc);
+    const double* yd = A(L.yd);
+    const double* xL = A(L.xL);
+    const double* zL = A(L.zL);
+    const double* s = A(L.s);
+    const double* dL = A(L.dL);
+    const double* dU = A(L.dU);
+    const double* vL = A(L.vL);
+    const double* vU = A(L.vU);
+    constexpr int NZ = LocalBlock<EN, EM>::NZ;
+    constexpr int NL = LocalBlock<EN, EM>::NL;
+    const int re = D.ePair + 2 * p;
+    const double sa = scE[re], sb = scE[re + 1], s1 = scI[2 * p], s3 = scI[2 * p + 1];
+    const double ya = sa * yc[re], yb = sb * yc[re + 1], y1 = s1 * yd[2 * p], y3 = s3 * yd[2 * p + 1];
+    const double tx = x[NS * i], ty = x[NS * i + 1];
+    // inequality slack elimination
+    if (ls) {
+      B.Ds1 = 1.0;
+      B.Ds3 = 1.0;
+    } else {
+      const int r1 = 2 * p, r3 = 2 * p + 1;
+      B.Ds1 = vL[r1] / (s[r1] - dL[r1]) + vU[r1] / (dU[r1] - s[r1]) + dw;
+      B.Ds3 = vL[r3] / (s[r3] - dL[r3]) + dw;
+    }
+    B.E1 = 1.0 / B.Ds1 + dc;
+    B.E3 = 1.0 / B.Ds3 + dc;
+    // Jacobian rows (z ordering: mu[0..EN), lam[0..EM)); padded entries are 0
+    double Aw[EM], Atb[EM], A0[EM], A1[EM];
+    for (int j = 0; j < EM; ++j) {
+      const bool on = j < em;
+      A0[j] = on ? Am[2 * j] : 0.0;
+      A1[j] = on ? Am[2 * j + 1] : 0.0;
+      Aw[j] = A0[j] * w[0] + A1[j] * w[1];
+      Atb[j] = on ? A0[j] * tx + A1[j] * ty - bm[j] : 0.0;
+    }
+    double G0[EN], G1[EN], gg[EN];
+    for (int j = 0; j < EN; ++j) {
+      const bool on = j < en;
+      G0[j] = on ? Gn[2 * j] : 0.0;
+      G1[j] = on ? Gn[2 * j + 1] : 0.0;
+      gg[j] = on ? gn[j] : 0.0;
+    }
+    for (int j = 0; j < EN; ++j) {
+      B.J1[j] = 0.0;
+      B.J3z[j] = -s3 * gg[j];
+    }
+    for (int j = 0; j < EM; ++j) {
+      B.J1[EN + j] = s1 * 2.0 * Aw[j];
+      B.J3z[EN + j] = s3 * Atb[j];
+    }
+    B.J3p[0] = s3 * w[0];
+    B.J3p[1] = s3 * w[1];
+    const double iE1 = 1.0 / B.E1, iE3 = 1.0 / B.E3;
+    // Hbar_zz
+    for (int r = 0; r < NZ; ++r)
+      for (int q = 0; q <= r; ++q)
+        B.K[B.pk(r, q)] = B.J1[r] * B.J1[q] * iE1 + B.J3z[r] * B.J3z[q] * iE3;
+    for (int j = 0; j < NZ; ++j) {
+      const bool is_mu = j < EN;
+      const int jj = is_mu ? j : j - EN;
+      const bool on = is_mu ? (jj < en) : (jj < em);
+      double dg;
+      if (!on) {
+        dg = 1.0;  // padding
+        for (int q = 0; q < NZ; ++q) {
+          if (q <= j) B.K[B.pk(j, q)] = 0.0;
+          else B.K[B.pk(q, j)] = 0.0;
+        }
+      } else if (ls) {
+        dg = 1.0;
+      } else {
+        const int vi = is_mu ? mu0 + jj : la0 + jj;
+        dg = zL[vi] / (x[vi] - xL[vi]) + dw;
+      }
+      B.K[B.pk(j, j)] += dg;
+    }
+    if (!ls) {
+      for (int r = 0; r < EM; ++r)
+        for (int q = 0; q <= r; ++q)
+          B.K[B.pk(EN + r, EN + q)] += y1 * 2.0 * (A0[r] * A0[q] + A1[r] * A1[q]);
+    }
+    // constraint rows c2a, c2b
+    for (int j = 0; j < EN; ++j) {
+      B.K[B.pk(NZ, j)] = sa * G0[j];
+      B.K[B.pk(NZ + 1, j)] = sb * G1[j];
+    }
+    for (int j = 0; j < EM; ++j) {
+      B.K[B.pk(NZ, EN + j)] = sa * (cs * A0[j] + sn * A1[j]);
+      B.K[B.pk(NZ + 1, EN + j)] = sb * (-sn * A0[j] + cs * A1[j]);
+    }
+    B.K[B.pk(NZ, NZ)] = -dc;
+    B.K[B.pk(NZ + 1, NZ)] = 0.0;
+    B.K[B.pk(NZ + 1, NZ + 1)] = -dc;
+    // coupling B = [Hbar_zp; Cp]
+    const double dRa = -sn * ya - cs * yb, dRb = cs * ya - sn * yb;  // dR^T/dth' y2
+    for (int r = 0; r < NZ; ++r) {
+      B.B[r][0] = B.J3z[r] * B.J3p[0] * iE3;
+      B.B[r][1] = B.J3z[r] * B.J3p[1] * iE3;
+      B.B[r][2] = 0.0;
+    }
+    if (!ls) {
+      for (int j = 0; j < EM; ++j) {
+        B.B[EN + j][0] += y3 * A0[j];
+        B.B[EN + j][1] += y3 * A1[j];
+        B.B[EN + j][2] += A0[j] * dRa + A1[j] * dRb;
+      }
+    }
+    B.B[NZ][0] = 0.0;
+    B.B[NZ][1] = 0.0;
+    B.B[NZ][2] = sa * (-sn * w[0] + cs * w[1]);
+    B.B[NZ + 1][0] = 0.0;
+    B.B[NZ + 1][1] = 0.0;
+    B.B[NZ + 1][2] = sb * (-cs * w[0] - sn * w[1]);
+    // direct p-p terms
+    B.Hpp[0] = B.J3p[0] * B.J3p[0] * iE3;
+    B.Hpp[1] = B.J3p[0] * B.J3p[1] * iE3;
+    B.Hpp[2] = B.J3p[1] * B.J3p[1] * iE3;
+    B.Hpp[3] = 0.0;
+    B.Hpp[4] = 0.0;
+    B.Hpp[5] = ls ? 0.0 : -(ya * (cs * w[0] + sn * w[1]) + yb * (-sn * w[0] + cs * w[1]));
+    (void)NL;
+  }
+
+  template <int EN, int EM>
+  HTP_HD void local_factor_sweep(bool ls, double dw, double dc, int& neg, int& zero) {
+    double* PS = A(L.pairS);
+    for (int p = c.lane; p < D.P; p += c.width) {
+      LocalBlock<EN, EM> B;
+      build_local<EN, EM>(B, p, ls, dw, dc);
+      B.factor();
+      neg += B.neg;
+      zero |= B.zero;
+      constexpr int NL = LocalBlock<EN, EM>::NL;
+      double S[6] = {0, 0, 0, 0, 0, 0};
+      for (int col = 0; col < 3; ++col) {
+        double v[NL];
+        for (int r = 0; r < NL; ++r) v[r] = B.B[r][col];
+        B.solve(v);
+        // S(:,col) = B' v
+        for (int row = 0; row <= col; ++row) {
+          double acc = 0.0;
+          for (int r = 0; r < NL; ++r) acc += B.B[r][row] * v[r];
+          // index map (row,col) -> xx0 xy1 yy2 xt3 yt4 tt5
+          const int idx = (col == 0) ? 0 : (col == 1 ? (row == 0 ? 1 : 2) : (row == 0 ? 3 : (row == 1 ? 4 : 5)));
+          S[idx] = acc;
+        }
+      }
+      for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
+    }
+  }
+
+  // rhs sweep: bx (x part), bs, bc, bd -> pairR (stage contributions)
+  template <int EN, int EM>
+  HTP_HD void local_rhs_sweep(bool ls, double dw, double dc, const double* bx, const double* bs,
+                              const double* bc, const double* bd) {
+    double* PR = A(L.pairR);
+    for (int p = c.lane; p < D.P; p += c.width) {
+      LocalBlock<EN, EM> B;
+      build_local<EN, EM>(B, p, ls, dw, dc);
+      B.factor();
+      constexpr int NZ = LocalBlock<EN, EM>::NZ;
+      constexpr int NL = LocalBlock<EN, EM>::NL;
+      int i, m, n, mu0, la0;
+      pair_index(p, i, m, n, mu0, la0);
+      const int em = D.eo[m], en = D.eb[n];
+      const double q1 = (bd[2 * p] + bs[2 * p] / B.Ds1) / B.E1;
+      const double q3 = (bd[2 * p + 1] + bs[2 * p + 1] / B.Ds3) / B.E3;
+      double v[NL];
+      for (int j = 0; j < EN; ++j) v[j] = (j < en ? bx[mu0 + j] : 0.0) + B.J1[j] * q1 + B.J3z[j] * q3;
+      for (int j = 0; j < EM; ++j) v[EN + j] = (j < em ? bx[la0 + j] : 0.0) + B.J1[EN + j] * q1 + B.J3z[EN + j] * q3;
+      const int re = D.ePair + 2 * p;
+      v[NZ] = bc[re];
+      v[NZ + 1] = bc[re + 1];
+      B.solve(v);
+      for (int col = 0; col < 3; ++col) {
+        double acc = 0.0;
+        for (int r = 0; r < NL; ++r) acc += B.B[r][col] * v[r];
+        PR[3 * p + col] = -acc + (col < 2 ? B.J3p[col] * q3 : 0.0);
+      }
+    }
+  }
+
+  template <int EN, int EM>
+  HTP_HD void local_back_sweep(bool ls, double dw, double dc, const double* bx, const double* bs,
+                               const double* bc, const double* bd, double* ox, double* os, double* oc,
+                               double* od) {
+    for (int p = c.lane; p < D.P; p += c.width) {
+      LocalBlock<EN, EM> B;
+      build_local<EN, EM>(B, p, ls, dw, dc);
+      B.factor();
+      constexpr int NZ = LocalBlock<EN, EM>::NZ;
+      constexpr int NL = LocalBlock<EN, EM>::NL;
+      int i, m, n, mu0, la0;
+      pair_index(p, i, m, n, mu0, la0);
+      const int em = D.eo[m], en = D.eb[n];
+      const double q1 = (bd[2 * p] + bs[2 * p] / B.Ds1) / B.E1;
+      const double q3 = (bd[2 * p + 1] + bs[2 * p + 1] / B.Ds3) / B.E3;
+      const double dpx = ox[NS * i], dpy = ox[NS * i + 1], dth = ox[NS * i + 3];
+      double v[NL];
+      for (int j = 0; j < EN; ++j) v[j] = (j < en ? bx[mu0 + j] : 0.0) + B.J1[j] * q1 + B.J3z[j] * q3;
+      for (int j = 0; j < EM; ++j) v[EN + j] = (j < em ? bx[la0 + j] : 0.0) + B.J1[EN + j] * q1 + B.J3z[EN + j] * q3;
+      const int re = D.ePair + 2 * p;
+      v[NZ] = bc[re];
+      v[NZ + 1] = bc[re + 1];
+      for (int r = 0; r < NL; ++r) v[r] -= B.B[r][0] * dpx + B.B[r][1] * dpy + B.B[r][2] * dth;
+      B.solve(v);
+      for (int j = 0; j < en; ++j) ox[mu0 + j] = v[j];
+      for (int j = 0; j < em; ++j) ox[la0 + j] = v[EN + j];
+      oc[re] = v[NZ];
+      oc[re + 1] = v[NZ + 1];
+      double j1 = 0.0, j3 = B.J3p[0] * dpx + B.J3p[1] * dpy;
+      for (int r = 0; r < NZ; ++r) {
+        j1 += B.J1[r] * v[r];
+        j3 += B.J3z[r] * v[r];
+      }
+      const double y1 = (j1 - bd[2 * p] - bs[2 * p] / B.Ds1) / B.E1;
+      const double y3 = (j3 - bd[2 * p + 1] - bs[2 * p + 1] / B.Ds3) / B.E3;
+      od[2 * p] = y1;
+      od[2 * p + 1] = y3;
+      os[2 * p] = (bs[2 * p] + y1) / B.Ds1;
+      os[2 * p + 1] = (bs[2 * p + 1] + y3) / B.Ds3;
+    }
+  }
+
+  HTP_HD bool uniform44() const {
+    for (int m = 0; m < D.M; ++m)
+      if (D.eo[m] != 4) return false;
+    for (int k = 0; k < D.K; ++k)
+      if (D.eb[k] != 4) return false;
+    return true;
+  }
+
+  // ---------------------------------------------------------- stage blocks
+  // block layout: [y 0..4 | x 5..9 | u 10,11 | tau 12]
+  HTP_HD void assemble_stage(int i, bool ls, double dw, double dc) {
+    const int N = D.N, nb = D.nb;
+    const double* x = A(L.x);
+    const double* xL = A(L.xL);
+    const double* xU = A(L.xU);
+    const double* zL = A(L.zL);
+    const double* zU = A(L.zU);
+    const double* scE = A(L.scE);
+    const double* yc = A(L.yc);
+    const double* PS = A(L.pairS);
+    double* K = A(L.Kst) + (int64_t)i * nb * nb;
+    const double dT = par(P_DT);
+    for (int q = 0; q < nb * nb; ++q) K[q] = 0.0;
+    auto add = [&](int r, int q, double v) {
+      K[r * nb + q] += v;
+      if (r != q) K[q * nb + r] += v;
+    };
+    for (int k = 0; k < NS; ++k) add(k, k, -dc);
+    const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
+    for (int k = 0; k < NS; ++k) add(k, NS + k, scE[rowbase + k]);
+    // variables of this block
+    int vidx[8];
+    int nv = (i < N - 1) ? D.nw : NS;
+    for (int k = 0; k < NS; ++k) vidx[k] = NS * i + k;
+    if (i < N - 1) {
+      vidx[5] = D.oU + NC * i;
+      vidx[6] = D.oU + NC * i + 1;
+      if (D.topt) vidx[7] = D.oTAU + i;
+    }
+    for (int a = 0; a < nv; ++a) {
+      const int q = vidx[a];
+      double dg;
+      if (ls) dg = 1.0;
+      else {
+        dg = dw;
+        if (finite_(xL[q])) dg += zL[q] / (x[q] - xL[q]);
+        if (finite_(xU[q])) dg += zU[q] / (xU[q] - x[q]);
+      }
+      add(NS + a, NS + a, dg);
+    }
+    for (int a = nv; a < D.nw; ++a) add(NS + a, NS + a, 1.0);  // padding (last stage)
+    if (!ls && i < N - 1) {
+      const double tau = tauv(x, i), h = dT * tau;
+      const double Qs00 = 2 * par(P_Q00), Qs01 = par(P_Q01) + par(P_Q10), Qs11 = 2 * par(P_Q11);
+      const double Rs00 = 2 * par(P_R00), Rs01 = par(P_R01) + par(P_R10), Rs11 = 2 * par(P_R11);
+      const int U0 = NS + 5, T0 = NS + 7, V0 = NS + 2;
+      add(U0, U0, sf * Qs00);
+      add(U0 + 1, U0, sf * Qs01);
+      add(U0 + 1, U0 + 1, sf * Qs11);
+      const double v = x[NS * i + 2];
+      add(V0, V0, sf * 2.0 * par(P_W00) * h * h);
+      if (D.topt) {
+        add(T0, T0, sf * 2.0 * par(P_W00) * v * v * dT * dT);
+        add(V0, T0, sf * 4.0 * par(P_W00) * v * dT * dT * tau);
+      }
+      if (i < N - 2) {
+        const double ih2 = 1.0 / (h * h);
+        add(U0, U0, sf * Rs00 * ih2);
+        add(U0 + 1, U0, sf * Rs01 * ih2);
+        add(U0 + 1, U0 + 1, sf * Rs11 * ih2);
+        if (D.topt) {
+          const double da = x[D.oU + NC * (i + 1)] - x[D.oU + NC * i];
+          const double dw_ = x[D.oU + NC * (i + 1) + 1] - x[D.oU + NC * i + 1];
+          const double Jv = (da * (par(P_R00) * da + par(P_R01) * dw_) + dw_ * (par(P_R10) * da + par(P_R11) * dw_)) * ih2;
+          add(T0, T0, sf * 6.0 * Jv / (tau * tau));
+          const double k2 = 2.0 * ih2 / tau;
+          add(U0, T0, sf * k2 * (Rs00 * da + Rs01 * dw_));
+          add(U0 + 1, T0, sf * k2 * (Rs01 * da + Rs11 * dw_));
+        }
+      }
+      if (i >= 1 && i - 1 < N - 2) {  // jerk_{i-1} on (u_i,u_i)
+        const double hp = dT * tauv(x, i - 1), ih2 = 1.0 / (hp * hp);
+        add(U0, U0, sf * Rs00 * ih2);
+        add(U0 + 1, U0, sf * Rs01 * ih2);
+        add(U0 + 1, U0 + 1, sf * Rs11 * ih2);
+      }
+      // dynamics Hessian of interval i:  sum_k (-yhat_k) d2F_k
+      double w[8], H[36], yy[5];
+      stage_w(x, i, w);
+      for (int k = 0; k < NS; ++k) yy[k] = -scE[D.eDyn + NS * i + k] * yc[D.eDyn + NS * i + k];
+      dynH(w, yy, H);
+      for (int r = 0; r < D.nw; ++r)
+        for (int q = 0; q <= r; ++q) add(NS + r, NS + q, H[r * (r + 1) / 2 + q]);
+    } else if (!ls && i >= 1 && i - 1 < N - 2) {
+      // last stage has no u; nothing else
+    }
+    // local-block Schur complements on (x, y, theta)
+    const int MK = D.M * D.K;
+    for (int q = 0; q < MK; ++q) {
+      const double* S = PS + 6 * (i * MK + q);
+      add(NS + 0, NS + 0, S[0]);
+      add(NS + 1, NS + 0, S[1]);
+      add(NS + 1, NS + 1, S[2]);
+      add(NS + 3, NS + 0, S[3]);
+      add(NS + 3, NS + 1, S[4]);
+      add(NS + 3, NS + 3, S[5]);
+    }
+    // terminal slack block (i == N-1): Hs = 10000 sf + dw
+    if (i == N - 1) {
+      const double Hs = ls ? 1.0 : 10000.0 * sf + dw;
+      for (int k = 0; k < NS; ++k) {
+        const double st = scE[D.eTerm + k];
+        const double Et = dc + st * st / Hs;
+        add(NS + k, NS + k, st * st / Et);
+      }
+    }
+    // off-diagonal block for i+1 (rows of block i+1, cols of block i)
+    if (i < N - 1) {
+      double* O = A(L.Off) + (int64_t)(i + 1) * nb * nb;
+      for (int q = 0; q < nb * nb; ++q) O[q] = 0.0;
+      double w[8], J[40];
+      stage_w(x, i, w);
+      dynJ(w, J);
+      for (int k = 0; k < NS; ++k) {
+        const double s_ = scE[D.eDyn + NS * i + k];
+        for (int j = 0; j < D.nw; ++j) O[k * nb + NS + j] = -s_ * J[k * D.nw + j];
+      }
+      if (!ls && i < N - 2) {
+        const double tau = tauv(x, i), h = dT * tau, ih2 = 1.0 / (h * h);
+        const double Rs00 = 2 * par(P_R00), Rs01 = par(P_R01) + par(P_R10), Rs11 = 2 * par(P_R11);
+        const int U0 = NS + 5, T0 = NS + 7;
+        O[U0 * nb + U0] = -sf * Rs00 * ih2;
+        O[U0 * nb + U0 + 1] = -sf * Rs01 * ih2;
+        O[(U0 + 1) * nb + U0] = -sf * Rs01 * ih2;
+        O[(U0 + 1) * nb + U0 + 1] = -sf * Rs11 * ih2;
+        if (D.topt) {
+          const double da = x[D.oU + NC * (i + 1)] - x[D.oU + NC * i];
+          const double dw_ = x[D.oU + NC * (i + 1) + 1] - x[D.oU + NC * i + 1];
+          const double k2 = -2.0 * ih2 / tau;
+          O[U0 * nb + T0] = sf * k2 * (Rs00 * da + Rs01 * dw_);
+          O[(U0 + 1) * nb + T0] = sf * k2 * (Rs01 * da + Rs11 * dw_);
+        }
+      }
+    }
+  }
+
+  // ----------------------------------------- Bunch-Kaufman on an LDS block
+  // a: n x n symmetric (full storage, row-major, stride nb); ip: pivots.
+  // On exit: unit L in the strict lower part, D on the (sub)diagonal,
+  // ip[k] >= 0: 1x1 pivot swapped with ip[k]; ip[k] = ip[k+1] = -(r+1): 2x2.
+  HTP_HD void bk_factor(double* a, int* ip, int n, int& neg, int& zero) {
+    const int nb = D.nb;
+    const double alpha = (1.0 + sqrt(17.0)) / 8.0;
+    double* sh = c.lds + 4 * NBMAX * NBMAX;  // scalars
+    int k = 0;
+    while (k < n) {
+      int kstep = 1, kp = k;
+      if (c.lane == 0) {
+        const double absakk = dabs(a[k * nb + k]);
+        int imax = k;
+        double colmax = 0.0;
+        for (int r = k + 1; r < n; ++r)
+          if (dabs(a[r * nb + k]) > colmax) { colmax = dabs(a[r * nb + k]); imax = r; }
+        if (dmax(absakk, colmax) == 0.0) {
+          kp = k; kstep = 1;
+        } else if (absakk >= alpha * colmax) {
+          kp = k; kstep = 1;
+        } else {
+          double rowmax = 0.0;
+          for (int j = k; j < n; ++j)
+            if (j != imax) rowmax = dmax(rowmax, dabs(a[imax * nb + j]));
+          if (absakk >= alpha * colmax * (colmax / rowmax)) { kp = k; kstep = 1; }
+          else if (dabs(a[imax * nb + imax]) >= alpha * rowmax) { kp = imax; kstep = 1; }
+          else { kp = imax; kstep = 2; }
+        }
+        sh[0] = kp;
+        sh[1] = kstep;
+      }
+      c.sync();
+      kp = (int)sh[0];
+      kstep = (int)sh[1];
+      c.sync();
+      const int kk = k + kstep - 1;
+      if (kp != kk) {  // LAPACK-style interchange of rows/cols kk, kp inside the trailing block A(k:n,k:n)
+        for (int j = k + c.lane; j < n; j += c.width) {
+          const double t = a[kk * nb + j];
+          a[kk * nb + j] = a[kp * nb + j];
+          a[kp * nb + j] = t;
+        }
+        c.sync();
+        for (int j = k + c.lane; j < n; j += c.width) {
+          const double t = a[j * nb + kk];
+          a[j * nb + kk] = a[j * nb + kp];
+          a[j * nb + kp] = t;
+        }
+        c.sync();
+      }
+      if (kstep == 1) {
+        const double d = a[k * nb + k];
+        if (d == 0.0) zero = 1;
+        if (d < 0.0) ++neg;
+        const double id = d != 0.0 ? 1.0 / d : 0.0;
+        const int m = n - k - 1;
+        for (int e = c.lane; e < m * m; e += c.width) {
+          const int r = k + 1 + e / m, q = k + 1 + e % m;
+          a[r * nb + q] -= a[r * nb + k] * a[q * nb + k] * id;
+        }
+        c.sync();
+        for (int r = k + 1 + c.lane; r < n; r += c.width) {
+          a[r * nb + k] *= id;
+          a[k * nb + r] = a[r * nb + k];
+        }
+        c.sync();
+      } else {
+        const double d11 = a[k * nb + k], d21 = a[(k + 1) * nb + k], d22 = a[(k + 1) * nb + k + 1];
+        const double det = d11 * d22 - d21 * d21;
+        if (det < 0.0) neg += 1;
+        else if (det > 0.0) neg += (d11 + d22 < 0.0) ? 2 : 0;
+        else zero = 1;
+        const double i11 = d22 / det, i22 = d11 / det, i21 = -d21 / det;
+        const int m = n - k - 2;
+        for (int e = c.lane; e < m * m; e += c.width) {
+          const int r = k + 2 + e / m, q = k + 2 + e % m;
+          const double ar1 = a[r * nb + k], ar2 = a[r * nb + k + 1];
+          const double aq1 = a[q * nb + k], aq2 = a[q * nb + k + 1];
+          const double l1 = ar1 * i11 + ar2 * i21, l2 = ar1 * i21 + ar2 * i22;
+          a[r * nb + q] -= l1 * aq1 + l2 * aq2;
+        }
+        c.sync();
+        for (int r = k + 2 + c.lane; r < n; r += c.width) {
+          const double ar1 = a[r * nb + k], ar2 = a[r * nb + k + 1];
+          const double l1 = ar1 * i11 + ar2 * i21, l2 = ar1 * i21 + ar2 * i22;
+          a[r * nb + k] = l1;
+          a[r * nb + k + 1] = l2;
+          a[k * nb + r] = l1;
+          a[(k + 1) * nb + r] = l2;
+        }
+        c.sync();
+      }
+      if (c.lane == 0) {
+        if (kstep == 1) ip[k] = kp;
+        else { ip[k] = -(kp + 1); ip[k + 1] = -(kp + 1); }
+      }
+      c.sync();
+      k += kstep;
+    }
+  }
+
+  // serial solve with a BK factor (one vector, executed by the calling lane)
+  HTP_HD void bk_solve_serial(const double* a, const int* ip, int n, double* b) const {
+    const int nb = D.nb;
+    int k = 0;
+    while (k < n) {  // forward: apply P then L^-1
+      if (ip[k] >= 0) {
+        const int kp = ip[k];
+        if (kp != k) { const double t = b[k]; b[k] = b[kp]; b[kp] = t; }
+        for (int r = k + 1; r < n; ++r) b[r] -= a[r * nb + k] * b[k];
+        k += 1;
+      } else {
+        const int kp = -ip[k] - 1;
+        if (kp != k + 1) { const double t = b[k + 1]; b[k + 1] = b[kp]; b[kp] = t; }
+        for (int r = k + 2; r < n; ++r) b[r] -= a[r * nb + k] * b[k] + a[r * nb + k + 1] * b[k + 1];
+        k += 2;
+      }
+    }
+    k = 0;
+    while (k < n) {  // D^-1
+      if (ip[k] >= 0) {
+        b[k] /= a[k * nb + k];
+        k += 1;
+      } else {
+        const double d11 = a[k * nb + k], d21 = a[(k + 1) * nb + k], d22 = a[(k + 1) * nb + k + 1];
+        const double det = d11 * d22 - d21 * d21;
+        const double b1 = b[k], b2 = b[k + 1];
+        b[k] = (d22 * b1 - d21 * b2) / det;
+        b[k + 1] = (-d21 * b1 + d11 * b2) / det;
+        k += 2;
+      }
+    }
+    k = n - 1;
+    while (k >= 0) {  // backward: L^-T then P^T
+      if (ip[k] >= 0) {
+        for (int r = k + 1; r < n; ++r) b[k] -= a[r * nb + k] * b[r];
+        const int kp = ip[k];
+        if (kp != k) { const double t = b[k]; b[k] = b[kp]; b[kp] = t; }
+        k -= 1;
+      } else {
+        for (int r = k + 1; r < n; ++r) {
+          b[k] -= a[r * nb + k] * b[r];
+          b[k - 1] -= a[r * nb + k - 1] * b[r];
+        }
+        const int kp = -ip[k] - 1;
+        if (kp != k) { const double t = b[k]; b[k] = b[kp]; b[kp] = t; }
+        k -= 2;
+      }
+    }
+  }
+
+  // ---------------------------------------------------------- factorization
+  // returns true if the inertia is the one IPOPT requires
+  HTP_HD void factorize(bool ls, double dw, double dc, int& neg_out, int& zero_out) {
+    const int N = D.N, nb = D.nb;
+    int neg = 0, zero = 0;
+    if (uniform44()) local_factor_sweep<4, 4>(ls, dw, dc, neg, zero);
+    else local_factor_sweep<MAXE, MAXE>(ls, dw, dc, neg, zero);
+    neg = c.isum(neg);
+    zero = c.isum(zero);
+    c.sync();
+    for (int i = c.lane; i < N; i += c.width) assemble_stage(i, ls, dw, dc);
+    c.sync();
+    // sequential block LDL^T over stages, in LDS
+    double* Acur = c.lds;                  // nb x nb
+    double* Dprev = c.lds + NBMAX * NBMAX; // nb x nb
+    double* Ybuf = c.lds + 2 * NBMAX * NBMAX;
+    int* ipp = c.ildsp;                    // pivots of Dprev
+    int* ipc = c.ildsp + NBMAX;
+    int sneg = 0, szero = 0;
+    for (int i = 0; i < N; ++i) {
+      const double* K = A(L.Kst) + (int64_t)i * nb * nb;
+      for (int e = c.lane; e < nb * nb; e += c.width) Acur[e] = K[e];
+      c.sync();
+      if (i > 0) {
+        const double* O = A(L.Off) + (int64_t)i * nb * nb;
+        // Y(:, j) = Dprev^-1 O(j, :)'   (lane j)
+        for (int j = c.lane; j < nb; j += c.width) {
+          double v[NBMAX];
+          for (int r = 0; r < nb; ++r) v[r] = O[j * nb + r];
+          bk_solve_serial(Dprev, ipp, nb, v);
+          for (int r = 0; r < nb; ++r) Ybuf[r * nb + j] = v[r];
+        }
+        c.sync();
+        // LD = O Dprev^-1 = Y' ; Acur -= O Y
+        double* LD = A(L.LD) + (int64_t)i * nb * nb;
+        for (int e = c.lane; e < nb * nb; e += c.width) {
+          const int r = e / nb, q = e % nb;
+          double acc = 0.0;
+          for (int t = 0; t < nb; ++t) acc += O[r * nb + t] * Ybuf[t * nb + q];
+          Acur[e] -= acc;
+          LD[e] = Ybuf[q * nb + r];
+        }
+        c.sync();
+      }
+      bk_factor(Acur, ipc, nb, sneg, szero);
+      double* F = A(L.fac) + (int64_t)i * nb * nb;
+      double* IP = A(L.ipiv) + (int64_t)i * nb;
+      for (int e = c.lane; e < nb * nb; e += c.width) {
+        F[e] = Acur[e];
+        Dprev[e] = Acur[e];
+      }
+      for (int e = c.lane; e < nb; e += c.width) {
+        IP[e] = ipc[e];
+        ipp[e] = ipc[e];
+      }
+      c.sync();
+    }
+    // terminal block contributes 5 negatives; inequality multipliers md negatives
+#ifdef HTP_HOST_DEBUG
+    printf("[dbg]   pairs neg=%d (exp %d) zero=%d stages neg=%d (exp %d) zero=%d\n", neg, 2 * D.P, zero, sneg, NS * N, szero);
+#endif
+    neg_out = neg + sneg + NS + D.md;
+    zero_out = zero + szero;
+  }
+
+  // solve K [ox; os; oc; od] = [bx; bs; bc; bd] with the current factorization
+  HTP_HD void kkt_solve(bool ls, double dw, double dc, const double* bx, const double* bs, const double* bc,
+                        const double* bd, double* ox, double* os, double* oc, double* od) {
+    const int N = D.N, nb = D.nb;
+    const bool u44 = uniform44();
+    if (u44) local_rhs_sweep<4, 4>(ls, dw, dc, bx, bs, bc, bd);
+    else local_rhs_sweep<MAXE, MAXE>(ls, dw, dc, bx, bs, bc, bd);
+    c.sync();
+    const double* PR = A(L.pairR);
+    const double* scE = A(L.scE);
+    double* V = A(L.V);
+    const int MK = D.M * D.K;
+    const double Hs = ls ? 1.0 : 10000.0 * sf + dw;
+    for (int i = c.lane; i < N; i += c.width) {
+      double* r = V + (int64_t)i * nb;
+      const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
+      for (int k = 0; k < NS; ++k) r[k] = bc[rowbase + k];
+      for (int k = 0; k < NS; ++k) r[NS + k] = bx[NS * i + k];
+      if (i < N - 1) {
+        r[NS + 5] = bx[D.oU + NC * i];
+        r[NS + 6] = bx[D.oU + NC * i + 1];
+        if (D.topt) r[NS + 7] = bx[D.oTAU + i];
+      } else {
+        for (int a = NS; a < D.nw; ++a) r[NS + a] = 0.0;
+        for (int k = 0; k < NS; ++k) {
+          const double st = scE[D.eTerm + k];
+          const double Et = dc + st * st / Hs;
+          r[NS + k] -= st / Et * (st * bx[D.oS + k] / Hs - bc[D.eTerm + k]);
+        }
+      }
+      for (int q = 0; q < MK; ++q) {
+        const int p = i * MK + q;
+        r[NS + 0] += PR[3 * p];
+        r[NS + 1] += PR[3 * p + 1];
+        r[NS + 3] += PR[3 * p + 2];
+      }
+    }
+    c.sync();
+    // forward: V_i -= LD_i V_{i-1}
+    for (int i = 1; i < N; ++i) {
+      const double* LD = A(L.LD) + (int64_t)i * nb * nb;
+      double* vi = V + (int64_t)i * nb;
+      const double* vp = V + (int64_t)(i - 1) * nb;
+      for (int r = c.lane; r < nb; r += c.width) {
+        double acc = 0.0;
+        for (int t = 0; t < nb; ++t) acc += LD[r * nb + t] * vp[t];
+        vi[r] -= acc;
+      }
+      c.sync();
+    }
+    // backward
+    double* X = A(L.X);
+    for (int i = N - 1; i >= 0; --i) {
+      double* xi = X + (int64_t)i * nb;
+      const double* vi = V + (int64_t)i * nb;
+      for (int r = c.lane; r < nb; r += c.width) {
+        double acc = vi[r];
+        if (i < N - 1) {
+          const double* O = A(L.Off) + (int64_t)(i + 1) * nb * nb;
+          const double* xn = X + (int64_t)(i + 1) * nb;
+          for (int t = 0; t < nb; ++t) acc -= O[t * nb + r] * xn[t];
+        }
+        xi[r] = acc;
+      }
+      c.sync();
+      if (c.lane == 0) {
+        const double* F = A(L.fac) + (int64_t)i * nb * nb;
+        const double* IPd = A(L.ipiv) + (int64_t)i * nb;
+        int ipv[NBMAX];
+        for (int t = 0; t < nb; ++t) ipv[t] = (int)IPd[t];
+        bk_solve_serial(F, ipv, nb, xi);
+      }
+      c.sync();
+    }
+    // scatter stage solution
+    for (int i = c.lane; i < N; i += c.width) {
+      const double* xi = X + (int64_t)i * nb;
+      const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
+      for (int k = 0; k < NS; ++k) oc[rowbase + k] = xi[k];
+      for (int k = 0; k < NS; ++k) ox[NS * i + k] = xi[NS + k];
+      if (i < N - 1) {
+        ox[D.oU + NC * i] = xi[NS + 5];
+        ox[D.oU + NC * i + 1] = xi[NS + 6];
+        if (D.topt) ox[D.oTAU + i] = xi[NS + 7];
+      } else {
+        for (int k = 0; k < NS; ++k) {
+          const double st = scE[D.eTerm + k];
+          const double Et = dc + st * st / Hs;
+          const double yt = (st * xi[NS + k] + st * bx[D.oS + k] / Hs - bc[D.eTerm + k]) / Et;
+          oc[D.eTerm + k] = yt;
+          ox[D.oS + k] = (bx[D.oS + k] - st * yt) / Hs;
+        }
+      }
+    }
+    c.sync();
+    if (u44) local_back_sweep<4, 4>(ls, dw, dc, bx, bs, bc, bd, ox, os, oc, od);
+    else local_back_sweep<MAXE, MAXE>(ls, dw, dc, bx, bs, bc, bd, ox, os, oc, od);
+    c.sync();
+  }
+  // ======================================================== IPM driver
+  // Mirrors oracle/ipm.py IpoptRestatement.solve line by line.
+  int nbL, nbU, nsL, nsU;  // counts of finite bounds
+
+  HTP_HD void count_bounds() {
+    const double* xL = A(L.xL);
+    const double* xU = A(L.xU);
+    const double* dU = A(L.dU);
+    int a = 0, b = 0, e = 0;
+    for (int q = c.lane; q < D.n; q += c.width) {
+      a += finite_(xL[q]);
+      b += finite_(xU[q]);
+    }
+    for (int r = c.lane; r < D.md; r += c.width) e += finite_(dU[r]);
+    nbL = c.isum(a);
+    nbU = c.isum(b);
+    nsL = D.md;
+    nsU = c.isum(e);
+  }
+
+  struct Err { double dual, comp, s_d, s_c, prim_b, prim_nlp; };
+
+  // grad Lagrangian (x part, w/o bound multipliers) -> rx
+  HTP_HD void grad_lag_into(double* out) {
+    eval_jt(A(L.x), A(L.yc), A(L.yd), out);
+    const double* gf = A(L.gf);
+    for (int q = c.lane; q < D.n; q += c.width) out[q] += gf[q];
+    c.sync();
+  }
+
+  HTP_HD Err errors(const double* gl, double mu_) const {
+    const double* x = A(L.x); const double* xL = A(L.xL); const double* xU = A(L.xU);
+    const double* zL = A(L.zL); const double* zU = A(L.zU);
+    const double* s = A(L.s); const double* dL = A(L.dL); const double* dU = A(L.dU);
+    const double* vL = A(L.vL); const double* vU = A(L.vU);
+    const double* yc = A(L.yc); const double* yd = A(L.yd);
+    const double* cc = A(L.c); const double* dd = A(L.d);
+    double dual = 0, comp = 0, zsum = 0, ysum = 0, pb = 0, pn = 0;
+    for (int q = c.lane; q < D.n; q += c.width) {
+      dual = dmax(dual, dabs(gl[q] - zL[q] + zU[q]));
+      if (finite_(xL[q])) { comp = dmax(comp, dabs((x[q] - xL[q]) * zL[q] - mu_)); zsum += dabs(zL[q]); }
+      if (finite_(xU[q])) { comp = dmax(comp, dabs((xU[q] - x[q]) * zU[q] - mu_)); zsum += dabs(zU[q]); }
+    }
+    for (int r = c.lane; r < D.md; r += c.width) {
+      dual = dmax(dual, dabs(-yd[r] - vL[r] + vU[r]));
+      comp = dmax(comp, dabs((s[r] - dL[r]) * vL[r] - mu_));
+      zsum += dabs(vL[r]);
+      if (finite_(dU[r])) { comp = dmax(comp, dabs((dU[r] - s[r]) * vU[r] - mu_)); zsum += dabs(vU[r]); }
+      ysum += dabs(yd[r]);
+      pb = dmax(pb, dabs(dd[r] - s[r]));
+      double v = dmax(0.0, dL[r] - dd[r]);
+      if (finite_(dU[r])) v = dmax(v, dd[r] - dU[r]);
+      pn = dmax(pn, v);
+    }
+    for (int r = c.lane; r < D.mc; r += c.width) {
+      ysum += dabs(yc[r]);
+      pb = dmax(pb, dabs(cc[r]));
+      pn = dmax(pn, dabs(cc[r]));
+    }
+    Err e;
+    e.dual = c.maxv(dual);
+    e.comp = c.maxv(comp);
+    zsum = c.sum(zsum);
+    ysum = c.sum(ysum);
+    e.prim_b = c.maxv(pb);
+    e.prim_nlp = c.maxv(pn);
+    const int nz = nbL + nbU + nsL + nsU, ny = D.mc + D.md;
+    e.s_d = dmax(o.s_max, (ysum + zsum) / (double)(ny + nz > 0 ? ny + nz : 1)) / o.s_max;
+    e.s_c = dmax(o.s_max, zsum / (double)(nz > 0 ? nz : 1)) / o.s_max;
+    return e;
+  }
+
+  // unscaled constraint violation of the original NLP at x (uses c, d arrays)
+  HTP_HD double unscaled_viol() const {
+    const double* cc = A(L.c); const double* dd = A(L.d);
+    const double* scE = A(L.scE); const double* scI = A(L.scI);
+    const double dmn = par(P_DMIN);
+    double v = 0;
+    for (int r = c.lane; r < D.mc; r += c.width) v = dmax(v, dabs(cc[r]) / scE[r]);
+    for (int r = c.lane; r < D.md; r += c.width) {
+      const double g = dd[r] / scI[r];
+      if ((r & 1) == 0) v = dmax(v, dmax(0.0 - g, g - 1.0));
+      else v = dmax(v, dmn - g);
+    }
+    return c.maxv(v);
+  }
+
+  HTP_HD double theta_of(const double* cc, const double* dd, const double* s) const {
+    double t = 0;
+    for (int r = c.lane; r < D.mc; r += c.width) t += dabs(cc[r]);
+    for (int r = c.lane; r < D.md; r += c.width) t += dabs(dd[r] - s[r]);
+    return c.sum(t);
+  }
+
+  // barrier function; returns +inf (as 1e308*10) if a slack is not positive
+  HTP_HD double barrier(const double* x, const double* s, double mu_) const {
+    const double* xL = A(L.xL); const double* xU = A(L.xU);
+    const double* dL = A(L.dL); const double* dU = A(L.dU);
+    const double kd = o.kappa_d * mu_;
+    double lg = 0.0, lin = 0.0;
+    int bad = 0;
+    for (int q = c.lane; q < D.n; q += c.width) {
+      const bool hl = finite_(xL[q]), hu = finite_(xU[q]);
+      if (hl) { const double v = x[q] - xL[q]; if (v <= 0) bad = 1; else lg += log(v); if (!hu) lin += v; }
+      if (hu) { const double v = xU[q] - x[q]; if (v <= 0) bad = 1; else lg += log(v); if (!hl) lin += v; }
+    }
+    for (int r = c.lane; r < D.md; r += c.width) {
+      const bool hu = finite_(dU[r]);
+      const double v = s[r] - dL[r];
+      if (v <= 0) bad = 1; else lg += log(v);
+      if (!hu) lin += v;
+      if (hu) { const double w = dU[r] - s[r]; if (w <= 0) bad = 1; else lg += log(w); }
+    }
+    bad = c.isum(bad);
+    lg = c.sum(lg);
+    lin = c.sum(lin);
+    if (bad) return HTP_INF;
+    return sf * eval_f(x) - mu_ * lg + kd * lin;
+  }
+
+  // barrier gradient -> gx (n), gs (md); needs gf current
+  HTP_HD void grad_barrier(double mu_, double* gx, double* gs) const {
+    const double* x = A(L.x); const double* xL = A(L.xL); const double* xU = A(L.xU);
+    const double* s = A(L.s); const double* dL = A(L.dL); const double* dU = A(L.dU);
+    const double* gf = A(L.gf);
+    const double kd = o.kappa_d * mu_;
+    for (int q = c.lane; q < D.n; q += c.width) {
+      const bool hl = finite_(xL[q]), hu = finite_(xU[q]);
+      double g = gf[q];
+      if (hl) g -= mu_ / (x[q] - xL[q]);
+      if (hu) g += mu_ / (xU[q] - x[q]);
+      if (hl && !hu) g += kd;
+      if (hu && !hl) g -= kd;
+      gx[q] = g;
+    }
+    for (int r = c.lane; r < D.md; r += c.width) {
+      const bool hu = finite_(dU[r]);
+      double g = -mu_ / (s[r] - dL[r]);
+      if (hu) g += mu_ / (dU[r] - s[r]);
+      else g += kd;
+      gs[r] = g;
+    }
+    c.sync();
+  }
+
+  HTP_HD double frac_primal(const double* dx, const double* ds) const {
+    const double* x = A(L.x); const double* xL = A(L.xL); const double* xU = A(L.xU);
+    const double* s = A(L.s); const double* dL = A(L.dL); const double* dU = A(L.dU);
+    double a = 1.0;
+    for (int q = c.lane; q < D.n; q += c.width) {
+      if (finite_(xL[q]) && dx[q] < 0) a = dmin(a, -tau * (x[q] - xL[q]) / dx[q]);
+      if (finite_(xU[q]) && -dx[q] < 0) a = dmin(a, -tau * (xU[q] - x[q]) / (-dx[q]));
+    }
+    for (int r = c.lane; r < D.md; r += c.width) {
+      if (ds[r] < 0) a = dmin(a, -tau * (s[r] - dL[r]) / ds[r]);
+      if (finite_(dU[r]) && -ds[r] < 0) a = dmin(a, -tau * (dU[r] - s[r]) / (-ds[r]));
+    }
+    return c.minv(a);
+  }
+
+  // bound-multiplier steps for (dx, ds) -> dzL, dzU, dvL, dvU ; returns alpha_dual
+  HTP_HD double dual_steps(const double* dx, const double* ds) {
+    const double* x = A(L.x); const double* xL = A(L.xL); const double* xU = A(L.xU);
+    const double* s = A(L.s); const double* dL = A(L.dL); const double* dU = A(L.dU);
+    const double* zL = A(L.zL); const double* zU = A(L.zU);
+    const double* vL = A(L.vL); const double* vU = A(L.vU);
+    double* dzL = A(L.dzL); double* dzU = A(L.dzU); double* dvL = A(L.dvL); double* dvU = A(L.dvU);
+    double a = 1.0;
+    for (int q = c.lane; q < D.n; q += c.width) {
+      double t = 0.0, u = 0.0;
+      if (finite_(xL[q])) { const double sl = x[q] - xL[q]; t = (mu - zL[q] * sl - zL[q] * dx[q]) / sl; if (t < 0) a = dmin(a, -tau * zL[q] / t); }
+      if (finite_(xU[q])) { const double su = xU[q] - x[q]; u = (mu - zU[q] * su + zU[q] * dx[q]) / su; if (u < 0) a = dmin(a, -tau * zU[q] / u); }
+      dzL[q] = t;
+      dzU[q] = u;
+    }
+    for (int r = c.lane; r < D.md; r += c.width) {
+      const double sl = s[r] - dL[r];
+      const double t = (mu - vL[r] * sl - vL[r] * ds[r]) / sl;
+      if (t < 0) a = dmin(a, -tau * vL[r] / t);
+      double u = 0.0;
+      if (finite_(dU[r])) { const double su = dU[r] - s[r]; u = (mu - vU[r] * su + vU[r] * ds[r]) / su; if (u < 0) a = dmin(a, -tau * vU[r] / u); }
+      dvL[r] = t;
+      dvU[r] = u;
+    }
+    c.sync();
+    return c.minv(a);
+  }
+
+  HTP_HD static bool cmp_le(double lhs, double rhs, double basval) {
+    return lhs - rhs <= 10.0 * 2.220446049250313e-16 * dabs(basval);
+  }
+
+  // factorization with inertia correction (IPOPT PDPerturbationHandler, simplified)
+  HTP_HD bool factor_ic(double& dw, double& dc) {
+    dw = 0.0;
+    dc = 0.0;
+    const int need = D.mc + D.md;
+    for (;;) {
+      int neg, zero;
+      factorize(false, dw, dc, neg, zero);
+      ++n_factor;
+#ifdef HTP_HOST_DEBUG
+      printf("[dbg] factor dw=%g dc=%g neg=%d need=%d zero=%d\n", dw, dc, neg, need, zero);
+#endif
+      if (neg == need && zero == 0) return true;
+      if (zero > 0 && dc == 0.0) { dc = o.dc_bar * pow(mu, o.kappa_c); continue; }
+      if (dw == 0.0) dw = (dw_last == 0.0) ? o.dw0 : dmax(o.dw_min, o.kw_minus * dw_last);
+      else dw = ((dw_last == 0.0 || 1e5 * dw_last < dw) ? o.kw_plus_bar : o.kw_plus) * dw;
+      if (dw > o.dw_max) return false;
+    }
+  }
+
+  // trial acceptability test (filter / Armijo); evaluates ct, dt at (xt, st)
+  HTP_HD bool acceptable(double a, const double* xt, const double* st, double phi, double theta, double gBD,
+                         bool ftype_ok, double& th_t, double& ph_t) {
+    double* ct = A(L.ct);
+    double* dtv = A(L.dt);
+    eval_cons(xt, ct, dtv);
+    th_t = theta_of(ct, dtv, st);
+    ph_t = barrier(xt, st, mu);
+    if (!(ph_t < 1e300) || th_t > theta_max) return false;
+    bool ok;
+    if (a > 0 && ftype_ok && theta <= theta_min) ok = cmp_le(ph_t - phi, o.eta_phi * a * gBD, phi);
+    else ok = cmp_le(th_t, (1 - o.gamma_theta) * theta, theta) || cmp_le(ph_t - phi, -o.gamma_phi * theta, phi);
+    if (!ok) return false;
+    for (int k = 0; k < nfilt; ++k)
+      if (!(th_t < f_th[k] || ph_t < f_ph[k])) return false;
+    return true;
+  }
+
+  HTP_HD void run(Result& res) {
+    initialize();
+    iterate(res);
+  }
+
+  HTP_HD void initialize() {
+    n_factor = 0;
+    dw_last = 0.0;
+    nfilt = 0;
+    set_bounds_and_x0();
+    compute_scaling();
+    relax_and_push();
+    double* x = A(L.x); double* s = A(L.s);
+    double* cc = A(L.c); double* dd = A(L.d);
+    eval_cons(x, cc, dd);
+    set_slack_bounds_and_push();
+    count_bounds();
+    {
+      const double* xL = A(L.xL); const double* xU = A(L.xU); const double* dU = A(L.dU);
+      double* zL = A(L.zL); double* zU = A(L.zU); double* vL = A(L.vL); double* vU = A(L.vU);
+      for (int q = c.lane; q < D.n; q += c.width) {
+        zL[q] = finite_(xL[q]) ? o.bound_mult_init_val : 0.0;
+        zU[q] = finite_(xU[q]) ? o.bound_mult_init_val : 0.0;
+      }
+      for (int r = c.lane; r < D.md; r += c.width) {
+        vL[r] = o.bound_mult_init_val;
+        vU[r] = finite_(dU[r]) ? o.bound_mult_init_val : 0.0;
+      }
+      double* yc = A(L.yc); double* yd = A(L.yd);
+      for (int r = c.lane; r < D.mc; r += c.width) yc[r] = 0.0;
+      for (int r = c.lane; r < D.md; r += c.width) yd[r] = 0.0;
+      c.sync();
+    }
+    eval_grad_f(x, A(L.gf), sf);
+    // least-squares multipliers
+    {
+      int neg, zero;
+      factorize(true, 0.0, 0.0, neg, zero);
+      ++n_factor;
+#ifdef HTP_HOST_DEBUG
+      printf("[dbg] LS factor neg=%d need=%d zero=%d\n", neg, D.mc + D.md, zero);
+#endif
+      if (neg == D.mc + D.md && zero == 0) {
+        double* bx = A(L.rx); double* bs = A(L.rs); double* bc = A(L.rc); double* bd = A(L.rd);
+        const double* gf = A(L.gf);
+        const double* zL = A(L.zL); const double* zU = A(L.zU); const double* vL = A(L.vL); const double* vU = A(L.vU);
+        for (int q = c.lane; q < D.n; q += c.width) bx[q] = -(gf[q] - zL[q] + zU[q]);
+        for (int r = c.lane; r < D.md; r += c.width) { bs[r] = -(-vL[r] + vU[r]); bd[r] = 0.0; }
+        for (int r = c.lane; r < D.mc; r += c.width) bc[r] = 0.0;
+        c.sync();
+        kkt_solve(true, 0.0, 0.0, bx, bs, bc, bd, A(L.dx), A(L.ds), A(L.dyc), A(L.dyd));
+        const double* a1 = A(L.dyc); const double* a2 = A(L.dyd);
+        double mx = 0.0;
+        for (int r = c.lane; r < D.mc; r += c.width) mx = dmax(mx, dabs(a1[r]));
+        for (int r = c.lane; r < D.md; r += c.width) mx = dmax(mx, dabs(a2[r]));
+        mx = c.maxv(mx);
+        if (mx <= o.constr_mult_init_max) {
+          double* yc = A(L.yc); double* yd = A(L.yd);
+          for (int r = c.lane; r < D.mc; r += c.width) yc[r] = a1[r];
+          for (int r = c.lane; r < D.md; r += c.width) yd[r] = a2[r];
+        }
+        c.sync();
+      }
+    }
+    mu = o.mu_init;
+    tau = dmax(o.tau_min, 1.0 - mu);
+    {
+      const double th0 = theta_of(cc, dd, s);
+      theta_max = 1e4 * dmax(1.0, th0);
+      theta_min = 1e-4 * dmax(1.0, th0);
+    }
+  }
+
+  HTP_HD void iterate(Result& res) {
+    double* x = A(L.x); double* s = A(L.s);
+    double* cc = A(L.c); double* dd = A(L.d);
+    int status = ST_MAXITER, it = 0, acc_count = 0;
+    double nlp_err = 0.0;
+    double* gl = A(L.rx);
+    for (it = 0; it <= o.max_iter; ++it) {
+      grad_lag_into(gl);
+      Err e0 = errors(gl, 0.0);
+      nlp_err = dmax(dmax(e0.dual / e0.s_d, e0.prim_nlp), e0.comp / e0.s_c);
+      const double uv = unscaled_viol();
+      if (nlp_err <= o.tol && e0.dual / sf <= o.dual_inf_tol && uv <= o.constr_viol_tol && e0.comp / sf <= o.compl_inf_tol) {
+        status = ST_SUCCESS;
+        break;
+      }
+      if (nlp_err <= o.acceptable_tol && e0.dual / sf <= o.acceptable_dual_inf_tol && uv <= o.acceptable_constr_viol_tol &&
+          e0.comp / sf <= o.acceptable_compl_inf_tol) {
+        if (++acc_count >= o.acceptable_iter) { status = ST_ACCEPTABLE; break; }
+      } else {
+        acc_count = 0;
+      }
+      if (it == o.max_iter) { status = ST_MAXITER; break; }
+      // monotone barrier update
+      for (;;) {
+        Err eb = errors(gl, mu);
+        const double berr = dmax(dmax(eb.dual / eb.s_d, eb.prim_b), eb.comp / eb.s_c);
+        if (berr > o.kappa_eps * mu) break;
+        const double nm = dmax(o.tol / 10.0, dmin(o.kappa_mu * mu, pow(mu, o.theta_mu)));
+        if (nm == mu) break;
+        mu = nm;
+        tau = dmax(o.tau_min, 1.0 - mu);
+        nfilt = 0;
+      }
+      // Newton rhs: rx = grad_barrier + J'y ; rs = gbs - yd ; rc = c ; rd = d - s  (negated below)
+      double* gbx = A(L.sx);   // scratch for barrier gradient
+      double* gbs = A(L.ss);
+      grad_barrier(mu, gbx, gbs);
+      double* rx = A(L.xt);    // use xt as rhs storage (x part), rebuilt below
+      double* rs = A(L.rs); double* rc = A(L.rc); double* rd = A(L.rd);
+      {
+        const double* gf = A(L.gf);
+        const double* yd = A(L.yd);
+        for (int q = c.lane; q < D.n; q += c.width) rx[q] = -(gl[q] - gf[q] + gbx[q]);
+        for (int r = c.lane; r < D.md; r += c.width) { rs[r] = -(gbs[r] - yd[r]); rd[r] = -(dd[r] - s[r]); }
+        for (int r = c.lane; r < D.mc; r += c.width) rc[r] = -cc[r];
+        c.sync();
+      }
+      double dw, dc;
+      if (!factor_ic(dw, dc)) { status = ST_STEPFAIL; break; }
+      if (dw > 0.0) dw_last = dw;
+      double* dx = A(L.dx); double* ds = A(L.ds); double* dyc = A(L.dyc); double* dyd = A(L.dyd);
+      kkt_solve(false, dw, dc, rx, rs, rc, rd, dx, ds, dyc, dyd);
+      // line search
+      const double phi = barrier(x, s, mu);
+      const double theta = theta_of(cc, dd, s);
+      double gBD = 0.0;
+      for (int q = c.lane; q < D.n; q += c.width) gBD += gbx[q] * dx[q];
+      for (int r = c.lane; r < D.md; r += c.width) gBD += gbs[r] * ds[r];
+      gBD = c.sum(gBD);
+      const double alpha_max = frac_primal(dx, ds);
+      double a_min = o.gamma_theta;
+      if (gBD < 0) {
+        a_min = dmin(o.gamma_theta, o.gamma_phi * theta / (-gBD));
+        if (theta <= theta_min) a_min = dmin(a_min, o.delta * pow(theta, o.s_theta) / pow(-gBD, o.s_phi));
+      }
+      a_min *= o.alpha_min_frac;
+      auto is_ftype = [&](double a) { return gBD < 0 && a * pow(-gBD, o.s_phi) > o.delta * pow(theta, o.s_theta); };
+      // keep the Newton rhs (x part) for SOC solves: copy into sx after gbx is consumed
+      double* rxk = A(L.sx);
+      for (int q = c.lane; q < D.n; q += c.width) rxk[q] = rx[q];
+      c.sync();
+      double* xt = A(L.xt); double* st = A(L.st);
+      double alpha = alpha_max, a_primal = alpha, a_test = alpha, th_t = 0, ph_t = 0;
+      bool accepted = false, soc_used = false, first = true;
+      while (alpha >= a_min) {
+        for (int q = c.lane; q < D.n; q += c.width) xt[q] = x[q] + alpha * dx[q];
+        for (int r = c.lane; r < D.md; r += c.width) st[r] = s[r] + alpha * ds[r];
+        c.sync();
+        if (acceptable(alpha, xt, st, phi, theta, gBD, is_ftype(alpha), th_t, ph_t)) {
+          accepted = true; a_primal = alpha; a_test = alpha;
+          break;
+        }
+        if (first && th_t >= theta && o.max_soc > 0) {
+          double* csoc = A(L.csoc); double* dsoc = A(L.dsoc);
+          const double* ct = A(L.ct); const double* dtv = A(L.dt);
+          for (int r = c.lane; r < D.mc; r += c.width) csoc[r] = alpha * cc[r] + ct[r];
+          for (int r = c.lane; r < D.md; r += c.width) dsoc[r] = alpha * (dd[r] - s[r]) + (dtv[r] - st[r]);
+          c.sync();
+          double th_old = theta;
+          double* sx = A(L.dzL);  // temporaries (dz arrays are recomputed after acceptance)
+          double* ss_ = A(L.dvL); double* syc = A(L.syc); double* syd = A(L.syd);
+          double* nrc = A(L.ct); double* nrd = A(L.dt);
+          for (int k = 0; k < o.max_soc; ++k) {
+            for (int r = c.lane; r < D.mc; r += c.width) nrc[r] = -csoc[r];
+            for (int r = c.lane; r < D.md; r += c.width) nrd[r] = -dsoc[r];
+            c.sync();
+            kkt_solve(false, dw, dc, rxk, rs, nrc, nrd, sx, ss_, syc, syd);
+            const double a_soc = frac_primal(sx, ss_);
+            for (int q = c.lane; q < D.n; q += c.width) xt[q] = x[q] + a_soc * sx[q];
+            for (int r = c.lane; r < D.md; r += c.width) st[r] = s[r] + a_soc * ss_[r];
+            c.sync();
+            double th_soc, ph_soc;
+            if (acceptable(alpha, xt, st, phi, theta, gBD, is_ftype(alpha), th_soc, ph_soc)) {
+              accepted = true; soc_used = true; a_primal = a_soc; a_test = alpha; ph_t = ph_soc;
+              for (int q = c.lane; q < D.n; q += c.width) dx[q] = sx[q];
+              for (int r = c.lane; r < D.md; r += c.width) { ds[r] = ss_[r]; dyd[r] = syd[r]; }
+              for (int r = c.lane; r < D.mc; r += c.width) dyc[r] = syc[r];
+              c.sync();
+              break;
+            }
+            if (th_soc > o.kappa_soc * th_old) break;
+            th_old = th_soc;
+            const double* ct2 = A(L.ct); const double* dt2 = A(L.dt);
+            for (int r = c.lane; r < D.mc; r += c.width) csoc[r] = a_soc * csoc[r] + ct2[r];
+            for (int r = c.lane; r < D.md; r += c.width) dsoc[r] = a_soc * dsoc[r] + (dt2[r] - st[r]);
+            c.sync();
+          }
+          if (accepted) break;
+        }
+        first = false;
+        alpha *= 0.5;
+      }
+      if (!accepted) { status = ST_RESTORATION; break; }
+      (void)soc_used;
+      // filter augmentation (uses the accepted trial's barrier value)
+      if (!(is_ftype(a_test) && cmp_le(ph_t - phi, o.eta_phi * a_test * gBD, phi))) {
+        if (nfilt < FMAX) { f_th[nfilt] = (1 - o.gamma_theta) * theta; f_ph[nfilt] = phi - o.gamma_phi * theta; ++nfilt; }
+        else { for (int k = 1; k < FMAX; ++k) { f_th[k - 1] = f_th[k]; f_ph[k - 1] = f_ph[k]; }
+               f_th[FMAX - 1] = (1 - o.gamma_theta) * theta; f_ph[FMAX - 1] = phi - o.gamma_phi * theta; }
+      }
+      const double a_dual = dual_steps(dx, ds);
+      {
+        double* zL = A(L.zL); double* zU = A(L.zU); double* vL = A(L.vL); double* vU = A(L.vU);
+        double* yc = A(L.yc); double* yd = A(L.yd);
+        const double* dzL = A(L.dzL); const double* dzU = A(L.dzU);
+        const double* dvL = A(L.dvL); const double* dvU = A(L.dvU);
+        const double* xL = A(L.xL); const double* xU = A(L.xU);
+        const double* dL = A(L.dL); const double* dU = A(L.dU);
+        const double ks = o.kappa_sigma;
+        for (int q = c.lane; q < D.n; q += c.width) {
+          x[q] += a_primal * dx[q];
+          if (finite_(xL[q])) { const double z = zL[q] + a_dual * dzL[q], v = x[q] - xL[q]; zL[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+          if (finite_(xU[q])) { const double z = zU[q] + a_dual * dzU[q], v = xU[q] - x[q]; zU[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+        }
+        for (int r = c.lane; r < D.md; r += c.width) {
+          s[r] += a_primal * ds[r];
+          yd[r] += a_primal * dyd[r];
+          { const double z = vL[r] + a_dual * dvL[r], v = s[r] - dL[r]; vL[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+          if (finite_(dU[r])) { const double z = vU[r] + a_dual * dvU[r], v = dU[r] - s[r]; vU[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+        }
+        for (int r = c.lane; r < D.mc; r += c.width) yc[r] += a_primal * dyc[r];
+        c.sync();
+      }
+      eval_cons(x, cc, dd);
+      eval_grad_f(x, A(L.gf), sf);
+    }
+    // honor_original_bounds: project into the unrelaxed bounds
+    project_original_bounds();
+    const double fobj = eval_f(x);
+    if (c.lane == 0) {
+      res.status = status;
+      res.iters = it;
+      res.n_factor = n_factor;
+      res.objective = fobj;
+      res.final_mu = mu;
+      res.nlp_error = nlp_err;
+      res.sf = sf;
+    }
+    c.sync();
+  }
+
+  // recompute original (unrelaxed) bounds and clip x
+  HTP_HD void project_original_bounds() {
+    double* x = A(L.x);
+    const double vmax = dabs(par(P_MAXV)), smax = dabs(par(P_MAXSTEER));
+    const double amax = dabs(par(P_MAXACC)), wmax = dabs(par(P_MAXSR));
+    const double twopi = 2.0 * M_PI;
+    for (int q = c.lane; q < D.n; q += c.width) {
+      double lo = -HTP_INF, hi = HTP_INF;
+      if (q < D.oU) {
+        const int k = q % NS;
+        if (k == 0) { lo = par(P_XLO); hi = par(P_XHI); }
+        if (k == 1) { lo = par(P_YLO); hi = par(P_YHI); }
+        if (k == 2) { lo = -vmax; hi = vmax; }
+        if (k == 3) { lo = -twopi; hi = twopi; }
+        if (k == 4) { lo = -smax; hi = smax; }
+      } else if (q < D.oMU) {
+        if ((q - D.oU) % 2 == 0) { lo = -amax; hi = amax; } else { lo = -wmax; hi = wmax; }
+      } else if (q < D.oTAU) {
+        lo = 0.0;
+      } else if (q < D.oS) {
+        lo = 0.05 / par(P_DT); hi = 1.0;
+      }
+      if (finite_(lo)) x[q] = dmax(x[q], lo);
+      if (finite_(hi)) x[q] = dmin(x[q], hi);
+    }
+    c.sync();
+  }
+};
+
+}  // namespace htp

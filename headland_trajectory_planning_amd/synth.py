@@ -1,0 +1,252 @@
+"""Deterministic synthetic headland-turn workload.
+
+Problem `pid` is drawn from Philox(key=[20251015, pid]) so a problem is
+identical for any batch composition and any GPU count.
+
+Geometry follows the reference's orchard model:
+* tree rows  ........... R/path_planner/utils/map_utils.py:45-61 (create_tree_rows)
+* exit / enter poses ... map_utils.py:228-271 (get_base_pose, NEAR_SIDE)
+* obstacles ............ R/path_planner/OGE_OBCA.py:306-373,477-677: a headland
+  boundary quad, the up/low bound quad and tree-row rectangles (SAFETY_BOUND 0.2),
+  trimmed / padded to exactly M convex quads (padding: far dummy quads, >= 50 m away)
+* warm start ........... the reference's Dubins fallback
+  (R/path_planner/OBCA_warm_start.py:166-174, pydubins shortest path) sampled to
+  exactly N poses, turned into [x, y, v, theta, steer] as
+  R/obca_py/util.py:62-113 does (v = dir*desired_v, steer = atan(L*kappa),
+  v[0]=v[-1]=steer[0]=0, heading wrapped + unwrapped).
+
+The headland boundary is placed behind the warm start's swept footprint with a
+random margin, so every instance starts collision-free and the boundary is
+close to active -- the regime the reference notebooks exercise.
+"""
+import math
+
+import numpy as np
+
+from . import geometry
+
+TWO_PI = 2.0 * math.pi
+
+MOWER = [[-1.84, 0.5], 1.0, 1.1]           # R/test/obca.ipynb (mowing preset)
+PRUNER = [[3.259, -0.175], 1.325, 0.3]     # R/test/obca.ipynb:133 (summer pruning)
+IMPLEMENTS = {"none": None, "mower": MOWER, "pruner": PRUNER}
+
+# Vehicle of SURVEY 8(d) / R/test/obca.ipynb:142
+VEHICLE = dict(max_steer=0.55, wheelbase=1.9, axle_to_front=2.85, axle_to_back=0.55, width=1.48)
+
+# OBCA weights of R/test/obca.ipynb:370-371,413-415
+DEFAULT_WEIGHTS = dict(dT=0.4, Q=np.diag([1.0, 1.0]), R=np.diag([0.1, 0.1]), W=np.diag([10.0, 0.1]))
+
+
+# ----------------------------------------------------------------- Dubins
+def _mod2pi(x):
+    return x - TWO_PI * math.floor(x / TWO_PI)
+
+
+def dubins_words(q0, q1, r):
+    """All admissible Dubins words (pydubins / Shkel-Lumelsky formulation).
+    Returns list of (name, (t, p, q)) in normalised (r=1) lengths."""
+    dx, dy = q1[0] - q0[0], q1[1] - q0[1]
+    D = math.hypot(dx, dy)
+    d = D / r
+    th = _mod2pi(math.atan2(dy, dx)) if D > 0 else 0.0
+    a = _mod2pi(q0[2] - th)
+    b = _mod2pi(q1[2] - th)
+    sa, sb, ca, cb = math.sin(a), math.sin(b), math.cos(a), math.cos(b)
+    cab = math.cos(a - b)
+    out = []
+    p2 = 2 + d * d - 2 * cab + 2 * d * (sa - sb)
+    if p2 >= 0:
+        t1 = math.atan2(cb - ca, d + sa - sb)
+        out.append(("LSL", (_mod2pi(-a + t1), math.sqrt(p2), _mod2pi(b - t1))))
+    p2 = 2 + d * d - 2 * cab + 2 * d * (sb - sa)
+    if p2 >= 0:
+        t1 = math.atan2(ca - cb, d - sa + sb)
+        out.append(("RSR", (_mod2pi(a - t1), math.sqrt(p2), _mod2pi(-b + t1))))
+    p2 = -2 + d * d + 2 * cab + 2 * d * (sa + sb)
+    if p2 >= 0:
+        p = math.sqrt(p2)
+        t2 = math.atan2(-ca - cb, d + sa + sb) - math.atan2(-2.0, p)
+        out.append(("LSR", (_mod2pi(-a + t2), p, _mod2pi(-_mod2pi(b) + t2))))
+    p2 = d * d - 2 + 2 * cab - 2 * d * (sa + sb)
+    if p2 >= 0:
+        p = math.sqrt(p2)
+        t2 = math.atan2(ca + cb, d - sa - sb) - math.atan2(2.0, p)
+        out.append(("RSL", (_mod2pi(a - t2), p, _mod2pi(b - t2))))
+    t0 = (6.0 - d * d + 2 * cab + 2 * d * (sa - sb)) / 8.0
+    if abs(t0) <= 1:
+        p = _mod2pi(TWO_PI - math.acos(t0))
+        t = _mod2pi(a - math.atan2(ca - cb, d - sa + sb) + p / 2.0)
+        out.append(("RLR", (t, p, _mod2pi(a - b - t + p))))
+    t0 = (6.0 - d * d + 2 * cab + 2 * d * (sb - sa)) / 8.0
+    if abs(t0) <= 1:
+        p = _mod2pi(TWO_PI - math.acos(t0))
+        t = _mod2pi(-a - math.atan2(ca - cb, d + sa - sb) + p / 2.0)
+        out.append(("LRL", (t, p, _mod2pi(_mod2pi(b) - a - t + p))))
+    return out
+
+
+def dubins_shortest(q0, q1, r):
+    words = dubins_words(q0, q1, r)
+    name, seg = min(words, key=lambda w: sum(w[1]))
+    return name, seg
+
+
+def dubins_sample(q0, r, name, seg, s):
+    """Pose + curvature at arc lengths s (metres) along a Dubins word."""
+    s = np.asarray(s, dtype=np.float64)
+    out = np.zeros((s.size, 4))
+    for j, sj in enumerate(s):
+        t = sj / r
+        x, y, th = 0.0, 0.0, q0[2]
+        kap = 0.0
+        for typ, ln in zip(name, seg):
+            st = min(t, ln)
+            if typ == "L":
+                x, y, th = x + math.sin(th + st) - math.sin(th), y - math.cos(th + st) + math.cos(th), th + st
+                kap = 1.0 / r
+            elif typ == "R":
+                x, y, th = x - math.sin(th - st) + math.sin(th), y + math.cos(th - st) - math.cos(th), th - st
+                kap = -1.0 / r
+            else:
+                x, y = x + math.cos(th) * st, y + math.sin(th) * st
+                kap = 0.0
+            t -= st
+            if t <= 0:
+                break
+        out[j] = (q0[0] + x * r, q0[1] + y * r, th, kap)
+    return out
+
+
+# ------------------------------------------------------------ angle helpers
+def wrap_angle(a):
+    """R/obca_py/util.py:7-13 (Python floored modulo)."""
+    return (np.asarray(a) + math.pi) % TWO_PI - math.pi
+
+
+def process_angle(raw):
+    """R/obca_py/util.py:16-43: wrap each angle, then unwrap the sequence."""
+    w = wrap_angle(np.asarray(raw, dtype=np.float64))
+    out = np.zeros_like(w)
+    if w.size:
+        out[0] = w[0]
+        for i in range(1, w.size):
+            out[i] = out[i - 1] + wrap_angle(w[i] - w[i - 1])
+    return out
+
+
+# ------------------------------------------------------------- polygon ops
+def _poly_at(poly, pose):
+    c, s = math.cos(pose[2]), math.sin(pose[2])
+    Rm = np.array([[c, -s], [s, c]])
+    return poly @ Rm.T + np.array(pose[:2])
+
+
+def _sat_gap(P, Q):
+    """Separating-axis gap between convex polygons (>0: disjoint)."""
+    best = -np.inf
+    for poly in (P, Q):
+        E = np.roll(poly, -1, axis=0) - poly
+        nrm = np.stack([E[:, 1], -E[:, 0]], axis=1)
+        nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+        pa, pb = P @ nrm.T, Q @ nrm.T
+        gap = np.maximum(pb.min(0) - pa.max(0), pa.min(0) - pb.max(0))
+        best = max(best, gap.max())
+    return best
+
+
+def _rect(x0, x1, y0, y1):
+    return np.array([[x0, y0], [x0, y1], [x1, y1], [x1, y0]], dtype=np.float64)
+
+
+# ---------------------------------------------------------------- instance
+def make_instance(pid, N=80, M=6, implement="none", key=20251015, **over):
+    """One OBCA instance (oracle/nlp.py instance format) for problem id `pid`."""
+    rng = np.random.Generator(np.random.Philox(key=[key, pid]))
+    veh = dict(VEHICLE)
+    r_min = veh["wheelbase"] / math.tan(veh["max_steer"])
+    body = geometry.body_rectangle(veh["axle_to_front"], veh["axle_to_back"], veh["width"])
+    polys = [body]
+    feat = IMPLEMENTS[implement]
+    if feat is not None:
+        polys.append(geometry.implement_rectangle(feat))
+
+    for _attempt in range(64):
+        rows = 8
+        row_w = rng.uniform(2.2, 3.5)
+        slope = math.radians(rng.uniform(-15.0, 15.0))
+        l_std = [0.0, 1.0][int(rng.integers(0, 2))]
+        tree_w, row_len = 0.3, 20.0
+        xs0 = np.array([row_w * math.tan(slope) * i + rng.uniform(-l_std, l_std) for i in range(rows)])
+        ys0 = row_w * np.arange(rows)
+        s_row = int(rng.integers(0, 5))
+        e_row = min(s_row + int(rng.integers(1, 4)), rows - 2)
+        exit_off = rng.uniform(-1.0, 1.0)
+        enter_off = rng.uniform(0.0, 3.66)
+        margin = rng.uniform(0.3, 1.0)
+
+        near = lambda r: np.array([(xs0[r] + xs0[r + 1]) / 2.0, (ys0[r] + ys0[r + 1]) / 2.0])
+        ps = near(s_row) + np.array([-1.0, 0.0]) * exit_off   # LEAVE, yaw = pi
+        pe = near(e_row) - np.array([1.0, 0.0]) * enter_off   # ENTER, yaw = 0
+        q0 = (ps[0], ps[1], math.pi)
+        q1 = (pe[0], pe[1], 0.0)
+        name, seg = dubins_shortest(q0, q1, r_min)
+        Lp = sum(seg) * r_min
+        smp = dubins_sample(q0, r_min, name, seg, np.linspace(0.0, Lp, N))
+        # footprint of the warm start (every pose, body + implements)
+        foot = [_poly_at(p, pose) for pose in smp[:, :3] for p in polys]
+        allpts = np.vstack(foot)
+        x_b = allpts[:, 0].min() - margin
+        obstacles = [_rect(x_b - 2.0, x_b, ys0.min() - 8.0, ys0.max() + 8.0)]
+        row_order = list(range(s_row + 1, e_row + 1)) + [s_row, e_row + 1]
+        for rr in [s_row - 1, e_row + 2]:
+            if 0 <= rr < rows:
+                row_order.append(rr)
+        row_rects = [_rect(xs0[r] - 0.2, xs0[r] + row_len + 0.2, ys0[r] - tree_w / 2, ys0[r] + tree_w / 2)
+                     for r in row_order]
+        up = _rect(xs0.min() - 8.0, xs0.max() + row_len + 8.0, ys0.max() + row_w, ys0.max() + row_w + 1.0)
+        cand = obstacles + row_rects + [up]
+        ok = all(_sat_gap(f, o) > 0.02 for o in cand[:M] for f in foot)
+        if ok:
+            break
+    cand = cand[:M]
+    k = 0
+    while len(cand) < M:  # far dummy quads
+        cx = ps[0] + 60.0 + 5.0 * k
+        cand.append(_rect(cx, cx + 1.0, ps[1] + 60.0, ps[1] + 61.0))
+        k += 1
+
+    dT = float(over.get("dT", DEFAULT_WEIGHTS["dT"]))
+    ds = Lp / (N - 1)
+    desired_v = min(ds / dT, 0.9)
+    traj = np.zeros((N, 5))
+    traj[:, 0], traj[:, 1] = smp[:, 0], smp[:, 1]
+    traj[:, 2] = desired_v
+    traj[:, 3] = process_angle(smp[:, 2])
+    traj[:, 4] = np.arctan(veh["wheelbase"] * smp[:, 3])
+    traj[0, 2] = traj[-1, 2] = 0.0
+    traj[0, 4] = 0.0
+
+    obs_A, obs_b = zip(*[geometry.polytope_halfspaces(o) for o in cand])
+    body_G, body_g = zip(*[geometry.polytope_halfspaces(p) for p in polys])
+    inst = dict(
+        init_traj=traj, obs_A=list(obs_A), obs_b=list(obs_b), body_G=list(body_G), body_g=list(body_g),
+        obstacles=cand, dT=dT, Q=DEFAULT_WEIGHTS["Q"].copy(), R=DEFAULT_WEIGHTS["R"].copy(),
+        W=DEFAULT_WEIGHTS["W"].copy(), wheelbase=veh["wheelbase"], max_steer=veh["max_steer"],
+        max_velocity=1.0, max_accel=1.0, max_steer_rate=0.7, min_dist=0.1,
+        x_bound=[-np.inf, np.inf], y_bound=[-np.inf, np.inf],
+        meta=dict(pid=pid, dubins=name, length=Lp, start=q0, goal=q1, s_row=s_row, e_row=e_row),
+    )
+    for kk, vv in over.items():
+        inst[kk] = vv
+    return inst
+
+
+CONFIGS = {
+    # name: (batch, N, M, implement)  -- BASELINE.json configs[0..4]
+    "A": (1, 40, 2, "none"),
+    "B": (256, 80, 6, "none"),
+    "C": (4096, 80, 6, "mower"),
+    "D": (32768, 80, 6, "none"),
+    "E": (4096, 160, 12, "pruner"),
+}

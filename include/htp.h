@@ -1,0 +1,97 @@
+/* htp.h -- C ABI of the MI355X-native headland-turn planner (libhtp.so).
+ *
+ * Drop-in boundary for the OBCA hot path of AgRoboticsResearch/
+ * headland_trajectory_planning.  The reference has no FFI of its own (it is
+ * pure Python over CasADi/IPOPT); these entry points replace:
+ *
+ *   htp_obca_solve_batch   OBCAOptimizer(...).solve()   R/obca_py/optimizer.py:77-138 (NLP
+ *                          construction) + :475-571 (nlpsol("ipopt") + solution slicing),
+ *                          batched over independent problems.
+ *   htp_obca_sizes         the decision-variable / constraint counts printed at
+ *                          R/obca_py/optimizer.py:490-498.
+ *
+ * Ownership: every array is caller-owned.  htp_obca_solve_batch takes HOST
+ * pointers (the library stages them to HBM); htp_obca_solve_batch_device takes
+ * DEVICE pointers already resident in HBM.  The library owns its workspace.
+ * Errors: 0 = OK, < 0 = API error (message via htp_last_error); per-problem
+ * solver status in htp_obca_result.status (HTP_STATUS_*).  No exceptions cross
+ * the ABI.  One htp_ctx per host thread.
+ */
+#ifndef HTP_H_
+#define HTP_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HTP_NPARAM 24
+/* per-problem parameter slots (double params[batch][HTP_NPARAM]) */
+enum {
+  HTP_P_DT = 0, HTP_P_Q00, HTP_P_Q01, HTP_P_Q10, HTP_P_Q11, HTP_P_R00, HTP_P_R01, HTP_P_R10, HTP_P_R11,
+  HTP_P_W00, HTP_P_W11, HTP_P_WHEELBASE, HTP_P_MAXSTEER, HTP_P_MAXV, HTP_P_MAXACC, HTP_P_MAXSR,
+  HTP_P_DMIN, HTP_P_XLO, HTP_P_XHI, HTP_P_YLO, HTP_P_YHI, HTP_P_HAS_INIT_CONTROL, HTP_P_HAS_INIT_DUAL
+};
+
+enum {
+  HTP_STATUS_SUCCESS = 0,            /* IPOPT "Solve_Succeeded" */
+  HTP_STATUS_ACCEPTABLE = 1,         /* "Solved_To_Acceptable_Level" */
+  HTP_STATUS_MAX_ITER = 2,           /* "Maximum_Iterations_Exceeded" */
+  HTP_STATUS_RESTORATION_FAILED = 3, /* line search failed (restoration phase not restated) */
+  HTP_STATUS_STEP_FAILED = 4,        /* "Error_In_Step_Computation" */
+  HTP_STATUS_BAD_INPUT = 5
+};
+
+typedef struct htp_ctx htp_ctx;
+
+/* One batch of OBCA problems sharing N (horizon), M obstacles, K bodies and
+ * the per-polytope edge counts.  Layouts are row-major, problem-major. */
+typedef struct {
+  int32_t batch, N, M, K, time_opt;   /* time_opt = (W[1][1] != 0), optimizer.py:109 */
+  const int32_t* obs_edges;           /* [M] edges of each obstacle polytope (<= 8)  */
+  const int32_t* body_edges;          /* [K] edges of each body polytope (<= 8)      */
+  const double* traj;                 /* [batch][N][5] init_traj (x, y, v, theta, steer) */
+  const double* obs_A;                /* [batch][sum obs_edges][2]  A of A x <= b    */
+  const double* obs_b;                /* [batch][sum obs_edges]                      */
+  const double* body_G;               /* [batch][sum body_edges][2] G of G x <= g    */
+  const double* body_g;               /* [batch][sum body_edges]                     */
+  const double* params;               /* [batch][HTP_NPARAM]                         */
+  const double* init_control;         /* nullable [batch][N-1][2]                    */
+  const double* init_mu;              /* nullable [batch][N][mu_count]               */
+  const double* init_lambda;          /* nullable [batch][N][lambda_count]           */
+} htp_obca_batch;
+
+typedef struct {
+  double* x;            /* [batch][n_var] optimal decision vector, optimizer.py layout */
+  double* objective;    /* [batch] f(x*) (unscaled) */
+  int32_t* status;      /* [batch] HTP_STATUS_* */
+  int32_t* iterations;  /* [batch] IPM iterations */
+  int32_t* n_factor;    /* [batch] KKT factorizations (inertia-correction retries included) */
+  double* nlp_error;    /* [batch] final scaled NLP error */
+} htp_obca_result;
+
+/* Sizes of one problem (n_var, n_eq, n_ineq as printed by optimizer.py:490-498)
+ * and the solver workspace in doubles. */
+int htp_obca_sizes(int32_t N, int32_t M, int32_t K, int32_t time_opt, const int32_t* obs_edges,
+                   const int32_t* body_edges, int64_t* n_var, int64_t* n_eq, int64_t* n_ineq,
+                   int64_t* ws_doubles);
+
+htp_ctx* htp_create(int32_t device);
+void htp_destroy(htp_ctx* ctx);
+const char* htp_last_error(htp_ctx* ctx);
+/* IPOPT option override by name (e.g. "tol", "max_iter"); 0 = OK */
+int htp_set_option(htp_ctx* ctx, const char* name, double value);
+
+/* Host buffers in, host buffers out (synchronous). */
+int htp_obca_solve_batch(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result* out);
+/* Device-resident buffers in/out; enqueued on `stream` (hipStream_t, may be
+ * NULL = default stream).  Not synchronised. */
+int htp_obca_solve_batch_device(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result* out, void* stream);
+/* Average duration (ms) of the last solve kernel measured with hipEvents on
+ * the launch stream (used by bench.py for the roofline). */
+double htp_last_kernel_ms(htp_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HTP_H_ */

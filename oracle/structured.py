@@ -1,0 +1,202 @@
+"""Oracle: structure-exploiting solve of the IPOPT augmented system for the
+OBCA NLP (oracle/nlp.py layout).  Same interface as ipm.DenseKKT.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).  It is the numpy blueprint
+of the HIP kernel's linear algebra and the CPU baseline at full config sizes.
+
+Elimination order (each step is a Schur complement, so by Sylvester's law the
+inertia of the full matrix is the sum of the inertias of the eliminated
+blocks -- the exact inertia IPOPT/MUMPS reports, whenever every eliminated
+block is nonsingular):
+
+ 1. inequality slacks s (Ds = Sigma_s + dw > 0)      -> +m_d positive
+    inequality multipliers y_d (-(1/Ds + dc) < 0)     -> +m_d negative
+    Hbar = W + Sigma_x + dw + Jd' diag(1/Ed) Jd
+ 2. "local blocks", eliminated onto their stage variables p:
+      collision pair (i,m,n): z = [mu_mn (e_n), lam_mn (e_m)], rows c2 (2 eq),
+                              p = (x_i, y_i, theta_i)
+      terminal:               z = slack_e (5), rows terminal (5 eq),
+                              p = x_{N-1}
+    Kloc = [Hbar_zz, Cz'; Cz, -dc]  (inertia by eigvalsh), B = [Hbar_zp; Cp]
+ 3. stage block-tridiagonal system, block i = [y_i (init / dyn_{i-1} rows),
+    x_i, u_i, tau_i]; block LDL^T (D_{i+1} = K_{i+1,i+1} - L D_i^{-1} L'),
+    inertia of each D_i by eigvalsh.
+"""
+import numpy as np
+import scipy.linalg as sla
+
+from .nlp import NS, NC
+
+
+def _eig_inertia(Ms):
+    """Inertia from a Bunch-Kaufman LDL^T (scale-robust, unlike eigvalsh)."""
+    _, d, _ = sla.ldl(Ms, lower=True)
+    pos = neg = zer = 0
+    i, n = 0, d.shape[0]
+    while i < n:
+        if i + 1 < n and d[i + 1, i] != 0.0:
+            ev = np.linalg.eigvalsh(d[i:i + 2, i:i + 2])
+            i += 2
+        else:
+            ev = [d[i, i]]
+            i += 1
+        for e in ev:
+            pos += e > 0
+            neg += e < 0
+            zer += e == 0
+    return int(pos), int(neg), int(zer)
+
+
+class StructuredKKT:
+    def __init__(self, nlp):
+        self.nlp = nlp
+        N = nlp.N
+        gL, gU = nlp.g_L, nlp.g_U
+        E = np.where(gL == gU)[0]
+        I = np.where(gL != gU)[0]
+        posE = -np.ones(nlp.m, dtype=int)
+        posE[E] = np.arange(E.size)
+        self.posE = posE
+        # local blocks: collision pairs (uniform sizes are not required)
+        self.loc = []
+        for p, (i, m, n, mu0, la0) in enumerate(nlp.pairs):
+            en, em = nlp.eb[n], nlp.eo[m]
+            z = np.concatenate([mu0 + np.arange(en), la0 + np.arange(em)])
+            r = nlp.gCol + 4 * p
+            self.loc.append((z, posE[[r + 1, r + 2]], np.array([NS * i, NS * i + 1, NS * i + 3])))
+        # terminal block
+        self.loc.append((nlp.oS + np.arange(NS), posE[nlp.gTerm + np.arange(NS)], NS * (N - 1) + np.arange(NS)))
+        # stage blocks
+        self.stage_vars, self.stage_rows = [], []
+        for i in range(N):
+            v = list(NS * i + np.arange(NS))
+            if i < N - 1:
+                v += [nlp.oU + NC * i, nlp.oU + NC * i + 1]
+                if nlp.topt:
+                    v.append(nlp.oTAU + i)
+            rows = np.arange(NS) if i == 0 else nlp.gDyn + NS * (i - 1) + np.arange(NS)
+            self.stage_vars.append(np.array(v))
+            self.stage_rows.append(posE[rows])
+        self.n_stage = sum(len(v) for v in self.stage_vars)
+
+    def factor(self, Wm, Sx, Ss, Jc, Jd, dw, dc):
+        nlp = self.nlp
+        Wm, Jc, Jd = Wm.tocsr(), Jc.tocsr(), Jd.tocsr()
+        n, mc, md = Wm.shape[0], Jc.shape[0], Jd.shape[0]
+        Ds = Ss + dw
+        Ed = 1.0 / Ds + dc
+        import scipy.sparse as sp
+        Hb = (Wm + sp.diags(Sx + dw) + Jd.T @ sp.diags(1.0 / Ed) @ Jd).tocsr()
+        pos, neg, zer = md, md, 0
+        Hd = Hb.toarray() if n <= 6000 else None
+        self._Hb, self._Jc, self._Jd, self._Ds, self._Ed, self._dc = Hb, Jc, Jd, Ds, Ed, dc
+        Jcd = Jc.toarray() if n <= 6000 else None
+
+        def hsub(r, c):
+            if Hd is not None:
+                return Hd[np.ix_(r, c)]
+            return Hb[r][:, c].toarray()
+
+        def jsub(r, c):
+            if Jcd is not None:
+                return Jcd[np.ix_(r, c)]
+            return Jc[r][:, c].toarray()
+
+        self.locfac = []
+        schur = {}
+        for (z, rows, p) in self.loc:
+            nz, nr = z.size, rows.size
+            K = np.zeros((nz + nr, nz + nr))
+            K[:nz, :nz] = hsub(z, z)
+            Cz = jsub(rows, z)
+            K[nz:, :nz] = Cz
+            K[:nz, nz:] = Cz.T
+            K[nz:, nz:] = -dc * np.eye(nr)
+            B = np.vstack([hsub(z, p), jsub(rows, p)])
+            a, b_, c_ = _eig_inertia(K)
+            pos, neg, zer = pos + a, neg + b_, zer + c_
+            if c_:
+                return pos, neg, zer
+            KiB = np.linalg.solve(K, B)
+            self.locfac.append((K, B, KiB))
+            key = tuple(p)
+            schur[key] = schur.get(key, 0.0) + B.T @ KiB
+        # stage blocks
+        N = nlp.N
+        self.D, self.Lo = [], []
+        prev = None
+        for i in range(N):
+            v, r = self.stage_vars[i], self.stage_rows[i]
+            nv, nr = v.size, r.size
+            K = np.zeros((nr + nv, nr + nv))
+            K[:nr, :nr] = -dc * np.eye(nr)
+            Jr = jsub(r, v)
+            K[:nr, nr:] = Jr
+            K[nr:, :nr] = Jr.T
+            K[nr:, nr:] = hsub(v, v)
+            # add the Schur complements of local blocks attached to this stage
+            for key, S in schur.items():
+                kk = np.array(key)
+                if np.all(np.isin(kk, v)):
+                    idx = nr + np.searchsorted(v, kk) if np.all(np.diff(v) > 0) else nr + np.array([list(v).index(q) for q in kk])
+                    K[np.ix_(idx, idx)] -= S
+            if prev is not None:
+                pv, pr, Dp = prev
+                # off-diagonal block: rows [y_i, v_i] x cols [y_{i-1}, v_{i-1}]
+                Off = np.zeros((nr + nv, pr.size + pv.size))
+                Off[:nr, pr.size:] = jsub(r, pv)
+                Off[nr:, pr.size:] = hsub(v, pv)
+                LD = np.linalg.solve(Dp, Off.T).T
+                K = K - LD @ Off.T
+                self.Lo.append((Off, LD))
+            a, b_, c_ = _eig_inertia(K)
+            pos, neg, zer = pos + a, neg + b_, zer + c_
+            self.D.append(K)
+            prev = (v, r, K)
+        return pos, neg, zer
+
+    def solve(self, bx, bs, bc, bd):
+        nlp = self.nlp
+        Jd, Ds, Ed = self._Jd, self._Ds, self._Ed
+        bxb = bx + Jd.T @ ((bd + bs / Ds) / Ed)
+        bcb = bc.copy()
+        # local block rhs
+        rloc = []
+        stage_rhs = {}
+        for (z, rows, p), (K, B, KiB) in zip(self.loc, self.locfac):
+            bl = np.concatenate([bxb[z], bcb[rows]])
+            Kib = np.linalg.solve(K, bl)
+            rloc.append(Kib)
+            for j, q in enumerate(p):
+                stage_rhs[q] = stage_rhs.get(q, 0.0) + B[:, j] @ Kib
+        # stage rhs
+        N = nlp.N
+        R = []
+        for i in range(N):
+            v, r = self.stage_vars[i], self.stage_rows[i]
+            rv = np.concatenate([bcb[r], np.array([bxb[q] - stage_rhs.get(q, 0.0) for q in v])])
+            R.append(rv)
+        # forward
+        V = [R[0]]
+        for i in range(1, N):
+            Off, LD = self.Lo[i - 1]
+            V.append(R[i] - LD @ V[i - 1])
+        X = [None] * N
+        X[N - 1] = np.linalg.solve(self.D[N - 1], V[N - 1])
+        for i in range(N - 2, -1, -1):
+            Off, LD = self.Lo[i]
+            X[i] = np.linalg.solve(self.D[i], V[i] - Off.T @ X[i + 1])
+        dx = np.zeros(nlp.n)
+        dyc = np.zeros(bc.size)
+        for i in range(N):
+            v, r = self.stage_vars[i], self.stage_rows[i]
+            dyc[r] = X[i][:r.size]
+            dx[v] = X[i][r.size:]
+        # local back-substitution
+        for (z, rows, p), (K, B, KiB), Kib in zip(self.loc, self.locfac, rloc):
+            w = Kib - KiB @ dx[p]
+            dx[z] = w[:z.size]
+            dyc[rows] = w[z.size:]
+        dyd = (Jd @ dx - bd - bs / Ds) / Ed
+        ds = (bs + dyd) / Ds
+        return dx, ds, dyc, dyd
