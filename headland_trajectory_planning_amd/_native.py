@@ -35,7 +35,7 @@ class ObcaResult(ctypes.Structure):
 
 
 EXPORTS = ["htp_obca_sizes", "htp_create", "htp_destroy", "htp_last_error", "htp_set_option",
-           "htp_obca_solve_batch", "htp_obca_solve_batch_device", "htp_last_kernel_ms"]
+           "htp_obca_solve_batch", "htp_obca_solve_batch_device", "htp_last_kernel_ms", "htp_last_cycles"]
 
 
 def _declare(lib):
@@ -56,6 +56,8 @@ def _declare(lib):
     lib.htp_obca_solve_batch_device.restype = ctypes.c_int
     lib.htp_last_kernel_ms.argtypes = [ctypes.c_void_p]
     lib.htp_last_kernel_ms.restype = ctypes.c_double
+    lib.htp_last_cycles.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
+    lib.htp_last_cycles.restype = ctypes.c_int
     return lib
 
 
@@ -218,6 +220,14 @@ class Context:
 
     def last_kernel_ms(self):
         return self.lib.htp_last_kernel_ms(self.ctx)
+
+    def last_cycles(self, batch):
+        """[batch, 6] shader-cycle counters: local sweeps, stage assembly,
+        stage chain, KKT solves, total, reserved."""
+        out = np.zeros((batch, 6), dtype=np.int64)
+        if self.lib.htp_last_cycles(self.ctx, out.ctypes.data, int(batch)) != 0:
+            raise RuntimeError(self.error())
+        return out
 
     def close(self):
         if self.ctx:

@@ -76,9 +76,18 @@ struct Layout {
   int64_t total;
 };
 
+// Everything a launch needs that is uniform over the batch (lives in
+// constant memory on the device; scalar-cached).
+struct Shape {
+  Dims D;
+  Layout L;
+  Options o;
+};
+
 struct Result {            // per problem
   int32_t status, iters, n_factor, pad;
   double objective, final_mu, nlp_error, sf;
+  int64_t cyc[6];          // shader cycles: local sweeps, stage assembly, stage chain, kkt solve, total, evals
 };
 
 enum Status { ST_SUCCESS = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_RESTORATION = 3, ST_STEPFAIL = 4,

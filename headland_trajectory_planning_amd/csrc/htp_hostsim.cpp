@@ -21,7 +21,7 @@ extern "C" int htp_hostsim_obca_solve(const htp_obca_batch* in, htp_obca_result*
   make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
   Layout L = make_layout(D);
   std::vector<double> ws((size_t)L.total);
-  std::vector<double> lds(4 * NBMAX * NBMAX + 8);
+  std::vector<double> lds(4 * NBMAX * NBMAX + 8 + 128);
   std::vector<int> ilds(2 * NBMAX);
   BatchView b{in->traj, in->obs_A, in->obs_b, in->body_G, in->body_g, in->params,
               in->init_control, in->init_mu, in->init_lambda};
@@ -30,7 +30,7 @@ extern "C" int htp_hostsim_obca_solve(const htp_obca_batch* in, htp_obca_result*
     c.lds = lds.data();
     c.ildsp = ilds.data();
     ProblemIn pin = problem_view(b, D, p);
-    ObcaSolver<HostLane> S(c, D, L, o, pin, ws.data());
+    ObcaSolver<HostLane, MAXE, MAXE> S(c, D, L, o, pin, ws.data());
     Result r{};
     S.run(r);
     for (int q = 0; q < D.n; ++q) out->x[(size_t)p * D.n + q] = ws[L.x + q];
@@ -52,7 +52,7 @@ extern "C" double htp_hostsim_debug_ws(const htp_obca_batch* in, int mode, doubl
   make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
   Layout L = make_layout(D);
   std::vector<double> ws((size_t)L.total);
-  std::vector<double> lds(4 * NBMAX * NBMAX + 8);
+  std::vector<double> lds(4 * NBMAX * NBMAX + 8 + 128);
   std::vector<int> ilds(2 * NBMAX);
   BatchView b{in->traj, in->obs_A, in->obs_b, in->body_G, in->body_g, in->params,
               in->init_control, in->init_mu, in->init_lambda};
@@ -60,7 +60,7 @@ extern "C" double htp_hostsim_debug_ws(const htp_obca_batch* in, int mode, doubl
   c.lds = lds.data();
   c.ildsp = ilds.data();
   ProblemIn pin = problem_view(b, D, 0);
-  ObcaSolver<HostLane> S(c, D, L, o, pin, ws.data());
+  ObcaSolver<HostLane, MAXE, MAXE> S(c, D, L, o, pin, ws.data());
   S.initialize();
   int neg = 0, zero = 0;
   if (mode == 1) S.factorize(false, dw, 0.0, neg, zero);

@@ -19,25 +19,31 @@ using namespace htp;
 
 namespace {
 
-constexpr int LDS_D = 4 * NBMAX * NBMAX + 8;
+constexpr int LDS_D = 4 * NBMAX * NBMAX + 8 + 2 * 64;
 
-__global__ __launch_bounds__(64) void obca_solve_kernel(Dims D, Layout L, Options o, BatchView b,
+template <int EN, int EM>
+__global__ __launch_bounds__(64) void obca_solve_kernel(const Shape* __restrict__ shp, BatchView b,
                                                         double* __restrict__ ws_all, int64_t ws_stride,
                                                         Result* __restrict__ res, double* __restrict__ xout,
                                                         int batch) {
-  __shared__ double lds[LDS_D];
-  __shared__ int ilds[2 * NBMAX];
+  __shared__ double lds_[LDS_D];
+  __shared__ int ilds_[2 * NBMAX];
+  DevWave::ld* lds = (DevWave::ld*)lds_;
+  DevWave::li* ilds = (DevWave::li*)ilds_;
   const int p = blockIdx.x;
   if (p >= batch) return;
   DevWave c{(int)threadIdx.x, lds, ilds};
-  ProblemIn in = problem_view(b, D, p);
+  using CS = DevWave::cst<Shape>;
+  CS* sh = (CS*)shp;
+  ProblemIn in = problem_view(b, sh->D, p);
   double* ws = ws_all + (int64_t)p * ws_stride;
-  ObcaSolver<DevWave> S(c, D, L, o, in, ws);
+  ObcaSolver<DevWave, EN, EM> S(c, sh->D, sh->L, sh->o, in, ws);
   Result r{};
   S.run(r);
   if (threadIdx.x == 0) res[p] = r;
-  const double* x = ws + L.x;
-  for (int q = threadIdx.x; q < D.n; q += 64) xout[(int64_t)p * D.n + q] = x[q];
+  const double* x = ws + sh->L.x;
+  const int n = sh->D.n;
+  for (int q = threadIdx.x; q < n; q += 64) xout[(int64_t)p * n + q] = x[q];
 }
 
 __global__ void unpack_results(const Result* __restrict__ r, int batch, double* obj, int32_t* st, int32_t* it,
@@ -61,6 +67,7 @@ struct htp_ctx {
   size_t ws_bytes = 0;
   void* scratch = nullptr;  // Result array
   size_t scratch_bytes = 0;
+  Shape* shape = nullptr;   // device copy of the launch-uniform shape
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0.0;
 };
@@ -117,6 +124,7 @@ void htp_destroy(htp_ctx* c) {
   if (!c) return;
   if (c->ws) (void)hipFree(c->ws);
   if (c->scratch) (void)hipFree(c->scratch);
+  if (c->shape) (void)hipFree(c->shape);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -132,6 +140,17 @@ int htp_set_option(htp_ctx* ctx, const char* name, double v) {
 
 double htp_last_kernel_ms(htp_ctx* c) { return c ? c->last_ms : 0.0; }
 
+// Diagnostic: per-problem phase cycle counters of the last solve ([batch][6] int64;
+// local sweeps, stage assembly, stage chain, KKT solves, total, reserved).
+int htp_last_cycles(htp_ctx* ctx, int64_t* out, int32_t batch) {
+  if (!ctx || !ctx->scratch) return -1;
+  std::vector<Result> r((size_t)batch);
+  HIPCHK(hipMemcpy(r.data(), ctx->scratch, sizeof(Result) * (size_t)batch, hipMemcpyDeviceToHost));
+  for (int p = 0; p < batch; ++p)
+    for (int k = 0; k < 6; ++k) out[(size_t)p * 6 + k] = r[(size_t)p].cyc[k];
+  return 0;
+}
+
 int htp_obca_solve_batch_device(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result* out, void* stream) {
   if (!ctx || !in || !out) return -1;
   const char* e = nullptr;
@@ -144,12 +163,22 @@ int htp_obca_solve_batch_device(htp_ctx* ctx, const htp_obca_batch* in, htp_obca
   const size_t need = (size_t)L.total * sizeof(double) * (size_t)in->batch;
   if (ensure(ctx, &ctx->ws, &ctx->ws_bytes, need)) return -1;
   if (ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, sizeof(Result) * (size_t)in->batch)) return -1;
+  if (!ctx->shape) HIPCHK(hipMalloc((void**)&ctx->shape, sizeof(Shape)));
+  Shape hs{D, L, ctx->opt};
   BatchView b{in->traj, in->obs_A, in->obs_b, in->body_G, in->body_g, in->params,
               in->init_control, in->init_mu, in->init_lambda};
   hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipMemcpyAsync(ctx->shape, &hs, sizeof(Shape), hipMemcpyHostToDevice, s));
   HIPCHK(hipEventRecord(ctx->ev0, s));
-  hipLaunchKernelGGL(obca_solve_kernel, dim3(in->batch), dim3(64), 0, s, D, L, ctx->opt, b, (double*)ctx->ws,
-                     (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
+  bool u44 = true;
+  for (int m = 0; m < D.M; ++m) u44 = u44 && D.eo[m] == 4;
+  for (int k = 0; k < D.K; ++k) u44 = u44 && D.eb[k] == 4;
+  if (u44)
+    hipLaunchKernelGGL((obca_solve_kernel<4, 4>), dim3(in->batch), dim3(64), 0, s, (const Shape*)ctx->shape, b,
+                       (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
+  else
+    hipLaunchKernelGGL((obca_solve_kernel<MAXE, MAXE>), dim3(in->batch), dim3(64), 0, s, (const Shape*)ctx->shape, b,
+                       (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1, s));
   hipLaunchKernelGGL(unpack_results, dim3((in->batch + 255) / 256), dim3(256), 0, s, (const Result*)ctx->scratch,

@@ -13,7 +13,8 @@ struct BatchView {  // plain copy of htp_obca_batch pointers (device or host)
   const double *traj, *obsA, *obsb, *bodyG, *bodyg, *params, *init_u, *init_mu, *init_la;
 };
 
-HTP_HD inline ProblemIn problem_view(const BatchView& b, const Dims& D, int64_t p) {
+template <class DD>
+HTP_HD inline ProblemIn problem_view(const BatchView& b, DD& D, int64_t p) {
   ProblemIn in;
   in.traj = b.traj + p * D.N * NS;
   in.obsA = b.obsA + p * D.TEo * 2;

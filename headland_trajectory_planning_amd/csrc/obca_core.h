@@ -19,6 +19,10 @@
 #include "htp_common.h"
 #include "dyn_gen.h"
 
+#ifndef HTP_FI
+#define HTP_FI __attribute__((always_inline))
+#endif
+
 namespace htp {
 
 struct ProblemIn {
@@ -33,13 +37,19 @@ struct ProblemIn {
   const double* init_la; // N x lam_count or null
 };
 
-HTP_HD inline double sq(double a) { return a * a; }
+HTP_HD HTP_FI inline double sq(double a) { return a * a; }
 HTP_HD inline bool finite_(double a) { return a > -1e300 && a < 1e300; }
 HTP_HD inline double dmax(double a, double b) { return a > b ? a : b; }
 HTP_HD inline double dmin(double a, double b) { return a < b ? a : b; }
 HTP_HD inline double dabs(double a) { return a < 0 ? -a : a; }
 
 constexpr double HTP_INF = __builtin_huge_val();
+
+#ifdef HTP_TRACE_ON
+#define HTP_TRACE(...) do { if (c.lane == 0) printf(__VA_ARGS__); } while (0)
+#else
+#define HTP_TRACE(...) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // Local (stage, obstacle m, body n) block:  z = [mu_mn (EN), lam_mn (EM)],
@@ -59,9 +69,9 @@ struct LocalBlock {
   double E1, E3, Ds1, Ds3;
   int neg, zero;
 
-  HTP_HD static int pk(int r, int c) { return r * (r + 1) / 2 + c; }
+  HTP_HD HTP_FI static int pk(int r, int c) { return r * (r + 1) / 2 + c; }
 
-  HTP_HD void factor() {  // unpivoted LDL^T of K (inertia = signs of D)
+  HTP_HD HTP_FI void factor() {  // unpivoted LDL^T of K (inertia = signs of D)
     neg = 0;
     zero = 0;
     for (int k = 0; k < NL; ++k) {
@@ -77,7 +87,7 @@ struct LocalBlock {
       }
     }
   }
-  HTP_HD void solve(double* v) const {  // in place K^-1 v
+  HTP_HD HTP_FI void solve(double* v) const {  // in place K^-1 v
     for (int k = 0; k < NL; ++k)
       for (int j = 0; j < k; ++j) v[k] -= K[pk(k, j)] * v[j];
     for (int k = 0; k < NL; ++k) v[k] /= K[pk(k, k)];
@@ -87,12 +97,18 @@ struct LocalBlock {
 };
 
 // ---------------------------------------------------------------------------
-template <class Ctx>
+template <class Ctx, int EN_ = 4, int EM_ = 4>
 struct ObcaSolver {
+  using gd = typename Ctx::gd;  // workspace / input arrays (HBM)
+  using ld = typename Ctx::ld;  // per-wave LDS scratch
+  using li = typename Ctx::li;
+  using CDims = typename Ctx::template cst<Dims>;
+  using CLayout = typename Ctx::template cst<Layout>;
+  using COptions = typename Ctx::template cst<Options>;
   Ctx& c;
-  const Dims& D;
-  const Layout& L;
-  const Options& o;
+  CDims& D;
+  CLayout& L;
+  COptions& o;
   const ProblemIn& in;
   double* ws;
 
@@ -100,20 +116,28 @@ struct ObcaSolver {
   double sf, mu, tau, dw_last;
   double theta_min, theta_max;
   int n_factor;
-  // filter (wave-uniform, small)
+  bool use_ric = false;
+  long long cyc[6];
+  // filter (wave-uniform): entries live in per-wave LDS (c.lds + FILT_OFF)
   static constexpr int FMAX = 64;
-  double f_th[FMAX], f_ph[FMAX];
+  static constexpr int FILT_OFF = 4 * NBMAX * NBMAX + 8;
+  ld* f_th;
+  ld* f_ph;
   int nfilt;
 
-  HTP_HD ObcaSolver(Ctx& c_, const Dims& D_, const Layout& L_, const Options& o_, const ProblemIn& in_, double* ws_)
-      : c(c_), D(D_), L(L_), o(o_), in(in_), ws(ws_) {}
+  HTP_HD HTP_FI ObcaSolver(Ctx& c_, CDims& D_, CLayout& L_, COptions& o_, const ProblemIn& in_, double* ws_)
+      : c(c_), D(D_), L(L_), o(o_), in(in_), ws(ws_) {
+    f_th = c.lds + FILT_OFF;
+    f_ph = c.lds + FILT_OFF + FMAX;
+  }
 
-  HTP_HD double* A(int64_t off) const { return ws + off; }
-  HTP_HD double par(int k) const { return in.par[k]; }
-  HTP_HD double tauv(const double* x, int i) const { return D.topt ? x[D.oTAU + i] : 1.0; }
+  HTP_HD HTP_FI gd* A(int64_t off) const { return (gd*)(ws + off); }
+  HTP_HD HTP_FI static const gd* gp(const double* p) { return (const gd*)p; }
+  HTP_HD HTP_FI double par(int k) const { return gp(in.par)[k]; }
+  HTP_HD HTP_FI double tauv(const gd* x, int i) const { return D.topt ? x[D.oTAU + i] : 1.0; }
 
   // pair p -> (i, m, n) and variable offsets
-  HTP_HD void pair_index(int p, int& i, int& m, int& n, int& mu0, int& la0) const {
+  HTP_HD HTP_FI void pair_index(int p, int& i, int& m, int& n, int& mu0, int& la0) const {
     n = p % D.K;
     int t = p / D.K;
     m = t % D.M;
@@ -123,28 +147,28 @@ struct ObcaSolver {
   }
 
   // stage w = [x_i (5), u_i (2), tau_i]
-  HTP_HD void stage_w(const double* x, int i, double* w) const {
+  HTP_HD HTP_FI void stage_w(const gd* x, int i, double* w) const {
     for (int k = 0; k < NS; ++k) w[k] = x[NS * i + k];
     w[5] = x[D.oU + NC * i];
     w[6] = x[D.oU + NC * i + 1];
     if (D.topt) w[7] = x[D.oTAU + i];
   }
-  HTP_HD void dynF(const double* w, double* F) const {
+  HTP_HD HTP_FI void dynF(const double* w, double* F) const {
     if (D.topt) dyn_F_rk2(w, par(P_DT), par(P_WHEELBASE), F);
     else dyn_F_euler(w, par(P_DT), par(P_WHEELBASE), F);
   }
-  HTP_HD void dynJ(const double* w, double* J) const {
+  HTP_HD HTP_FI void dynJ(const double* w, double* J) const {
     if (D.topt) dyn_J_rk2(w, par(P_DT), par(P_WHEELBASE), J);
     else dyn_J_euler(w, par(P_DT), par(P_WHEELBASE), J);
   }
-  HTP_HD void dynH(const double* w, const double* y, double* H) const {
+  HTP_HD HTP_FI void dynH(const double* w, const double* y, double* H) const {
     if (D.topt) dyn_H_rk2(w, par(P_DT), par(P_WHEELBASE), y, H);
     else dyn_H_euler(w, par(P_DT), par(P_WHEELBASE), y, H);
   }
 
   // ======================================================== objective
   // f (unscaled) -- optimizer.py:447-473
-  HTP_HD double stage_obj(const double* x, int i) const {
+  HTP_HD HTP_FI double stage_obj(const gd* x, int i) const {
     const int N = D.N;
     const double dT = par(P_DT);
     double f = 0.0;
@@ -163,13 +187,13 @@ struct ObcaSolver {
       for (int k = 0; k < NS; ++k) f += 5000.0 * sq(x[D.oS + k]);
     return f;
   }
-  HTP_HD double eval_f(const double* x) const {
+  HTP_HD HTP_FI double eval_f(const gd* x) const {
     double f = 0.0;
     for (int i = c.lane; i < D.N; i += c.width) f += stage_obj(x, i);
     return c.sum(f);
   }
   // scaled gradient (sf * grad f) into g (all n entries written)
-  HTP_HD void eval_grad_f(const double* x, double* g, double scale) const {
+  HTP_HD HTP_FI void eval_grad_f(const gd* x, gd* g, double scale) const {
     const int N = D.N;
     const double dT = par(P_DT);
     const double Qs00 = 2 * par(P_Q00), Qs01 = par(P_Q01) + par(P_Q10), Qs11 = 2 * par(P_Q11);
@@ -208,11 +232,11 @@ struct ObcaSolver {
 
   // ======================================================== constraints
   // scaled c (equality) and d (inequality) at x (optimizer.py:356-425)
-  HTP_HD void pair_geom(const double* x, int p, double* w, double& cs, double& sn,
+  HTP_HD HTP_FI void pair_geom(const gd* x, int p, double* w, double& cs, double& sn,
                         int& i, int& m, int& n, int& mu0, int& la0) const {
     pair_index(p, i, m, n, mu0, la0);
     const int em = D.eo[m];
-    const double* Am = in.obsA + 2 * D.offo[m];
+    const gd* Am = gp(in.obsA) + 2 * D.offo[m];
     w[0] = w[1] = 0.0;
     for (int j = 0; j < em; ++j) {
       w[0] += Am[2 * j] * x[la0 + j];
@@ -223,15 +247,15 @@ struct ObcaSolver {
     sn = sin(th);
   }
 
-  HTP_HD void pair_cons(const double* x, int p, double* out4) const {
+  HTP_HD HTP_FI void pair_cons(const gd* x, int p, double* out4) const {
     double w[2], cs, sn;
     int i, m, n, mu0, la0;
     pair_geom(x, p, w, cs, sn, i, m, n, mu0, la0);
     const int em = D.eo[m], en = D.eb[n];
-    const double* Am = in.obsA + 2 * D.offo[m];
-    const double* bm = in.obsb + D.offo[m];
-    const double* Gn = in.bodyG + 2 * D.offb[n];
-    const double* gn = in.bodyg + D.offb[n];
+    const gd* Am = gp(in.obsA) + 2 * D.offo[m];
+    const gd* bm = gp(in.obsb) + D.offo[m];
+    const gd* Gn = gp(in.bodyG) + 2 * D.offb[n];
+    const gd* gn = gp(in.bodyg) + D.offb[n];
     double c2a = cs * w[0] + sn * w[1], c2b = -sn * w[0] + cs * w[1], c3 = 0.0;
     for (int j = 0; j < en; ++j) {
       const double mu = x[mu0 + j];
@@ -247,13 +271,13 @@ struct ObcaSolver {
     out4[3] = c3;
   }
 
-  HTP_HD void eval_cons(const double* x, double* cc, double* dd) const {
+  HTP_HD HTP_FI void eval_cons(const gd* x, gd* cc, gd* dd) const {
     const int N = D.N;
-    const double* scE = A(L.scE);
-    const double* scI = A(L.scI);
+    const gd* scE = A(L.scE);
+    const gd* scI = A(L.scI);
     for (int i = c.lane; i < N; i += c.width) {
       if (i == 0)
-        for (int k = 0; k < NS; ++k) cc[k] = scE[k] * (x[k] - in.traj[k]);
+        for (int k = 0; k < NS; ++k) cc[k] = scE[k] * (x[k] - gp(in.traj)[k]);
       if (i < N - 1) {
         double w[8], F[5];
         stage_w(x, i, w);
@@ -265,7 +289,7 @@ struct ObcaSolver {
       } else {
         for (int k = 0; k < NS; ++k) {
           const int r = D.eTerm + k;
-          cc[r] = scE[r] * (x[NS * i + k] - in.traj[NS * i + k] + x[D.oS + k]);
+          cc[r] = scE[r] * (x[NS * i + k] - gp(in.traj)[NS * i + k] + x[D.oS + k]);
         }
       }
     }
@@ -282,11 +306,11 @@ struct ObcaSolver {
   }
 
   // J_c' yc + J_d' yd (x part) into out (scaled rows; yc, yd multipliers of scaled rows)
-  HTP_HD void eval_jt(const double* x, const double* yc, const double* yd, double* out) {
+  HTP_HD HTP_FI void eval_jt(const gd* x, const gd* yc, const gd* yd, gd* out) {
     const int N = D.N;
-    const double* scE = A(L.scE);
-    const double* scI = A(L.scI);
-    double* pr = A(L.pairR);
+    const gd* scE = A(L.scE);
+    const gd* scI = A(L.scI);
+    gd* pr = A(L.pairR);
     for (int q = c.lane; q < D.n; q += c.width) out[q] = 0.0;
     c.sync();
     for (int p = c.lane; p < D.P; p += c.width) {
@@ -294,10 +318,10 @@ struct ObcaSolver {
       int i, m, n, mu0, la0;
       pair_geom(x, p, w, cs, sn, i, m, n, mu0, la0);
       const int em = D.eo[m], en = D.eb[n];
-      const double* Am = in.obsA + 2 * D.offo[m];
-      const double* bm = in.obsb + D.offo[m];
-      const double* Gn = in.bodyG + 2 * D.offb[n];
-      const double* gn = in.bodyg + D.offb[n];
+      const gd* Am = gp(in.obsA) + 2 * D.offo[m];
+      const gd* bm = gp(in.obsb) + D.offo[m];
+      const gd* Gn = gp(in.bodyG) + 2 * D.offb[n];
+      const gd* gn = gp(in.bodyg) + D.offb[n];
       const int re = D.ePair + 2 * p;
       const double ya = scE[re] * yc[re], yb = scE[re + 1] * yc[re + 1];
       const double y1 = scI[2 * p] * yd[2 * p], y3 = scI[2 * p + 1] * yd[2 * p + 1];
@@ -351,11 +375,11 @@ struct ObcaSolver {
   }
 
   // ======================================================== setup
-  HTP_HD void set_bounds_and_x0() {
+  HTP_HD HTP_FI void set_bounds_and_x0() {
     const int N = D.N;
-    double* x = A(L.x);
-    double* xL = A(L.xL);
-    double* xU = A(L.xU);
+    gd* x = A(L.x);
+    gd* xL = A(L.xL);
+    gd* xU = A(L.xU);
     const double vmax = dabs(par(P_MAXV)), smax = dabs(par(P_MAXSTEER));
     const double amax = dabs(par(P_MAXACC)), wmax = dabs(par(P_MAXSR));
     const double twopi = 2.0 * M_PI;
@@ -363,7 +387,7 @@ struct ObcaSolver {
       double lo = -HTP_INF, hi = HTP_INF, v0 = 0.0;
       if (q < D.oU) {
         const int i = q / NS, k = q % NS;
-        v0 = in.traj[q];
+        v0 = gp(in.traj)[q];
         if (k == 0) { lo = par(P_XLO); hi = par(P_XHI); }
         if (k == 1) { lo = par(P_YLO); hi = par(P_YHI); }
         if (k == 2) { lo = -vmax; hi = vmax; }
@@ -372,13 +396,13 @@ struct ObcaSolver {
         (void)i;
       } else if (q < D.oMU) {
         const int j = q - D.oU;
-        v0 = in.init_u ? in.init_u[j] : 0.0;
+        v0 = in.init_u ? gp(in.init_u)[j] : 0.0;
         if (j % 2 == 0) { lo = -amax; hi = amax; } else { lo = -wmax; hi = wmax; }
       } else if (q < D.oLAM) {
-        v0 = in.init_mu ? in.init_mu[q - D.oMU] : 0.1;
+        v0 = in.init_mu ? gp(in.init_mu)[q - D.oMU] : 0.1;
         lo = 0.0;
       } else if (q < D.oTAU) {
-        v0 = in.init_la ? in.init_la[q - D.oLAM] : 0.1;
+        v0 = in.init_la ? gp(in.init_la)[q - D.oLAM] : 0.1;
         lo = 0.0;
       } else if (q < D.oS) {
         v0 = 1.0;
@@ -393,17 +417,17 @@ struct ObcaSolver {
   }
 
   // gradient-based scaling at the user x0 (IPOPT nlp_scaling_method default)
-  HTP_HD void compute_scaling() {
+  HTP_HD HTP_FI void compute_scaling() {
     const int N = D.N;
-    const double* x = A(L.x);
-    double* g = A(L.gf);
+    const gd* x = A(L.x);
+    gd* g = A(L.gf);
     eval_grad_f(x, g, 1.0);
     double mg = 0.0;
     for (int q = c.lane; q < D.n; q += c.width) mg = dmax(mg, dabs(g[q]));
     mg = c.maxv(mg);
     sf = mg > o.scaling_max_gradient ? dmax(o.scaling_min_value, o.scaling_max_gradient / mg) : 1.0;
-    double* scE = A(L.scE);
-    double* scI = A(L.scI);
+    gd* scE = A(L.scE);
+    gd* scI = A(L.scI);
     auto scl = [&](double rm) {
       return rm > o.scaling_max_gradient ? dmax(o.scaling_min_value, o.scaling_max_gradient / rm) : 1.0;
     };
@@ -428,10 +452,10 @@ struct ObcaSolver {
       int i, m, n, mu0, la0;
       pair_geom(x, p, w, cs, sn, i, m, n, mu0, la0);
       const int em = D.eo[m], en = D.eb[n];
-      const double* Am = in.obsA + 2 * D.offo[m];
-      const double* bm = in.obsb + D.offo[m];
-      const double* Gn = in.bodyG + 2 * D.offb[n];
-      const double* gn = in.bodyg + D.offb[n];
+      const gd* Am = gp(in.obsA) + 2 * D.offo[m];
+      const gd* bm = gp(in.obsb) + D.offo[m];
+      const gd* Gn = gp(in.bodyG) + 2 * D.offb[n];
+      const gd* gn = gp(in.bodyg) + D.offb[n];
       double r1 = 0, ra = 0, rb = 0, r3 = 0;
       const double tx = x[NS * i], ty = x[NS * i + 1];
       for (int j = 0; j < em; ++j) {
@@ -457,10 +481,10 @@ struct ObcaSolver {
     c.sync();
   }
 
-  HTP_HD void relax_and_push() {
-    double* x = A(L.x);
-    double* xL = A(L.xL);
-    double* xU = A(L.xU);
+  HTP_HD HTP_FI void relax_and_push() {
+    gd* x = A(L.x);
+    gd* xL = A(L.xL);
+    gd* xU = A(L.xU);
     const double rf = o.bound_relax_factor;
     for (int q = c.lane; q < D.n; q += c.width) {
       double lo = xL[q], hi = xU[q];
@@ -474,7 +498,7 @@ struct ObcaSolver {
     c.sync();
   }
 
-  HTP_HD double push(double v, double lo, double hi, bool hl, bool hu) const {
+  HTP_HD HTP_FI double push(double v, double lo, double hi, bool hl, bool hu) const {
     double pl = hl ? o.bound_push * dmax(1.0, dabs(lo)) : 0.0;
     double pu = hu ? o.bound_push * dmax(1.0, dabs(hi)) : 0.0;
     if (hl && hu) {
@@ -487,14 +511,14 @@ struct ObcaSolver {
   }
 
   // inequality-row bounds: c1 in [0,1], c3 in [dmin, inf), relaxed and scaled
-  HTP_HD void set_slack_bounds_and_push() {
+  HTP_HD HTP_FI void set_slack_bounds_and_push() {
     const double rf = o.bound_relax_factor;
     double dmn = par(P_DMIN);
-    double* s = A(L.s);
-    double* dL = A(L.dL);
-    double* dU = A(L.dU);
-    const double* d = A(L.d);
-    const double* scI = A(L.scI);
+    gd* s = A(L.s);
+    gd* dL = A(L.dL);
+    gd* dU = A(L.dU);
+    const gd* d = A(L.d);
+    const gd* scI = A(L.scI);
     for (int r = c.lane; r < D.md; r += c.width) {
       double lo, hi;
       if ((r & 1) == 0) { lo = 0.0; hi = 1.0; } else { lo = dmn; hi = HTP_INF; }
@@ -513,27 +537,27 @@ struct ObcaSolver {
   // ======================================================== KKT assembly
   // mode_ls: least-squares multiplier system (W=0, identity x/s blocks)
   template <int EN, int EM>
-  HTP_HD void build_local(LocalBlock<EN, EM>& B, int p, bool ls, double dw, double dc) const {
-    const double* x = A(L.x);
+  HTP_HD HTP_FI void build_local(LocalBlock<EN, EM>& B, int p, bool ls, double dw, double dc) const {
+    const gd* x = A(L.x);
     double w[2], cs, sn;
     int i, m, n, mu0, la0;
     pair_geom(x, p, w, cs, sn, i, m, n, mu0, la0);
     const int em = D.eo[m], en = D.eb[n];
-    const double* Am = in.obsA + 2 * D.offo[m];
-    const double* bm = in.obsb + D.offo[m];
-    const double* Gn = in.bodyG + 2 * D.offb[n];
-    const double* gn = in.bodyg + D.offb[n];
-    const double* scE = A(L.scE);
-    const double* scI = A(L.scI);
-    const double* yc = A(L.yc);
-    const double* yd = A(L.yd);
-    const double* xL = A(L.xL);
-    const double* zL = A(L.zL);
-    const double* s = A(L.s);
-    const double* dL = A(L.dL);
-    const double* dU = A(L.dU);
-    const double* vL = A(L.vL);
-    const double* vU = A(L.vU);
+    const gd* Am = gp(in.obsA) + 2 * D.offo[m];
+    const gd* bm = gp(in.obsb) + D.offo[m];
+    const gd* Gn = gp(in.bodyG) + 2 * D.offb[n];
+    const gd* gn = gp(in.bodyg) + D.offb[n];
+    const gd* scE = A(L.scE);
+    const gd* scI = A(L.scI);
+    const gd* yc = A(L.yc);
+    const gd* yd = A(L.yd);
+    const gd* xL = A(L.xL);
+    const gd* zL = A(L.zL);
+    const gd* s = A(L.s);
+    const gd* dL = A(L.dL);
+    const gd* dU = A(L.dU);
+    const gd* vL = A(L.vL);
+    const gd* vU = A(L.vU);
     constexpr int NZ = LocalBlock<EN, EM>::NZ;
     constexpr int NL = LocalBlock<EN, EM>::NL;
     const int re = D.ePair + 2 * p;
@@ -649,8 +673,8 @@ struct ObcaSolver {
   }
 
   template <int EN, int EM>
-  HTP_HD void local_factor_sweep(bool ls, double dw, double dc, int& neg, int& zero) {
-    double* PS = A(L.pairS);
+  HTP_HD HTP_FI void local_factor_sweep(bool ls, double dw, double dc, int& neg, int& zero) {
+    gd* PS = A(L.pairS);
     for (int p = c.lane; p < D.P; p += c.width) {
       LocalBlock<EN, EM> B;
       build_local<EN, EM>(B, p, ls, dw, dc);
@@ -678,9 +702,9 @@ struct ObcaSolver {
 
   // rhs sweep: bx (x part), bs, bc, bd -> pairR (stage contributions)
   template <int EN, int EM>
-  HTP_HD void local_rhs_sweep(bool ls, double dw, double dc, const double* bx, const double* bs,
-                              const double* bc, const double* bd) {
-    double* PR = A(L.pairR);
+  HTP_HD HTP_FI void local_rhs_sweep(bool ls, double dw, double dc, const gd* bx, const gd* bs,
+                              const gd* bc, const gd* bd) {
+    gd* PR = A(L.pairR);
     for (int p = c.lane; p < D.P; p += c.width) {
       LocalBlock<EN, EM> B;
       build_local<EN, EM>(B, p, ls, dw, dc);
@@ -708,9 +732,9 @@ struct ObcaSolver {
   }
 
   template <int EN, int EM>
-  HTP_HD void local_back_sweep(bool ls, double dw, double dc, const double* bx, const double* bs,
-                               const double* bc, const double* bd, double* ox, double* os, double* oc,
-                               double* od) {
+  HTP_HD HTP_FI void local_back_sweep(bool ls, double dw, double dc, const gd* bx, const gd* bs,
+                               const gd* bc, const gd* bd, gd* ox, gd* os, gd* oc,
+                               gd* od) {
     for (int p = c.lane; p < D.P; p += c.width) {
       LocalBlock<EN, EM> B;
       build_local<EN, EM>(B, p, ls, dw, dc);
@@ -749,7 +773,7 @@ struct ObcaSolver {
     }
   }
 
-  HTP_HD bool uniform44() const {
+  HTP_HD HTP_FI bool uniform44() const {
     for (int m = 0; m < D.M; ++m)
       if (D.eo[m] != 4) return false;
     for (int k = 0; k < D.K; ++k)
@@ -759,17 +783,17 @@ struct ObcaSolver {
 
   // ---------------------------------------------------------- stage blocks
   // block layout: [y 0..4 | x 5..9 | u 10,11 | tau 12]
-  HTP_HD void assemble_stage(int i, bool ls, double dw, double dc) {
+  HTP_HD HTP_FI void assemble_stage(int i, bool ls, double dw, double dc) {
     const int N = D.N, nb = D.nb;
-    const double* x = A(L.x);
-    const double* xL = A(L.xL);
-    const double* xU = A(L.xU);
-    const double* zL = A(L.zL);
-    const double* zU = A(L.zU);
-    const double* scE = A(L.scE);
-    const double* yc = A(L.yc);
-    const double* PS = A(L.pairS);
-    double* K = A(L.Kst) + (int64_t)i * nb * nb;
+    const gd* x = A(L.x);
+    const gd* xL = A(L.xL);
+    const gd* xU = A(L.xU);
+    const gd* zL = A(L.zL);
+    const gd* zU = A(L.zU);
+    const gd* scE = A(L.scE);
+    const gd* yc = A(L.yc);
+    const gd* PS = A(L.pairS);
+    gd* K = A(L.Kst) + (int64_t)i * nb * nb;
     const double dT = par(P_DT);
     for (int q = 0; q < nb * nb; ++q) K[q] = 0.0;
     auto add = [&](int r, int q, double v) {
@@ -848,7 +872,7 @@ struct ObcaSolver {
     // local-block Schur complements on (x, y, theta)
     const int MK = D.M * D.K;
     for (int q = 0; q < MK; ++q) {
-      const double* S = PS + 6 * (i * MK + q);
+      const gd* S = PS + 6 * (i * MK + q);
       add(NS + 0, NS + 0, S[0]);
       add(NS + 1, NS + 0, S[1]);
       add(NS + 1, NS + 1, S[2]);
@@ -867,7 +891,7 @@ struct ObcaSolver {
     }
     // off-diagonal block for i+1 (rows of block i+1, cols of block i)
     if (i < N - 1) {
-      double* O = A(L.Off) + (int64_t)(i + 1) * nb * nb;
+      gd* O = A(L.Off) + (int64_t)(i + 1) * nb * nb;
       for (int q = 0; q < nb * nb; ++q) O[q] = 0.0;
       double w[8], J[40];
       stage_w(x, i, w);
@@ -899,10 +923,10 @@ struct ObcaSolver {
   // a: n x n symmetric (full storage, row-major, stride nb); ip: pivots.
   // On exit: unit L in the strict lower part, D on the (sub)diagonal,
   // ip[k] >= 0: 1x1 pivot swapped with ip[k]; ip[k] = ip[k+1] = -(r+1): 2x2.
-  HTP_HD void bk_factor(double* a, int* ip, int n, int& neg, int& zero) {
+  HTP_HD HTP_FI void bk_factor(ld* a, li* ip, int n, int& neg, int& zero) {
     const int nb = D.nb;
     const double alpha = (1.0 + sqrt(17.0)) / 8.0;
-    double* sh = c.lds + 4 * NBMAX * NBMAX;  // scalars
+    ld* sh = c.lds + 4 * NBMAX * NBMAX;  // scalars
     int k = 0;
     while (k < n) {
       int kstep = 1, kp = k;
@@ -997,113 +1021,427 @@ struct ObcaSolver {
     }
   }
 
-  // serial solve with a BK factor (one vector, executed by the calling lane)
-  HTP_HD void bk_solve_serial(const double* a, const int* ip, int n, double* b) const {
+  // out = A^{-1} from a BK factor (lane-parallel over (row, col) entries)
+  HTP_HD HTP_FI void bk_inverse(const ld* a, const li* ip, int n, ld* out) {
     const int nb = D.nb;
+    for (int e = c.lane; e < nb * nb; e += c.width) out[e] = ((e / nb) == (e % nb) && e / nb < n) ? 1.0 : 0.0;
+    c.sync();
     int k = 0;
-    while (k < n) {  // forward: apply P then L^-1
+    while (k < n) {  // P then L^-1 on all columns
       if (ip[k] >= 0) {
         const int kp = ip[k];
-        if (kp != k) { const double t = b[k]; b[k] = b[kp]; b[kp] = t; }
-        for (int r = k + 1; r < n; ++r) b[r] -= a[r * nb + k] * b[k];
+        if (kp != k) {
+          for (int q = c.lane; q < n; q += c.width) { const double t = out[k * nb + q]; out[k * nb + q] = out[kp * nb + q]; out[kp * nb + q] = t; }
+          c.sync();
+        }
+        const int m = n - k - 1;
+        for (int e = c.lane; e < m * n; e += c.width) {
+          const int r = k + 1 + e / n, q = e % n;
+          out[r * nb + q] -= a[r * nb + k] * out[k * nb + q];
+        }
+        c.sync();
         k += 1;
       } else {
         const int kp = -ip[k] - 1;
-        if (kp != k + 1) { const double t = b[k + 1]; b[k + 1] = b[kp]; b[kp] = t; }
-        for (int r = k + 2; r < n; ++r) b[r] -= a[r * nb + k] * b[k] + a[r * nb + k + 1] * b[k + 1];
+        if (kp != k + 1) {
+          for (int q = c.lane; q < n; q += c.width) { const double t = out[(k + 1) * nb + q]; out[(k + 1) * nb + q] = out[kp * nb + q]; out[kp * nb + q] = t; }
+          c.sync();
+        }
+        const int m = n - k - 2;
+        for (int e = c.lane; e < m * n; e += c.width) {
+          const int r = k + 2 + e / n, q = e % n;
+          out[r * nb + q] -= a[r * nb + k] * out[k * nb + q] + a[r * nb + k + 1] * out[(k + 1) * nb + q];
+        }
+        c.sync();
         k += 2;
       }
     }
-    k = 0;
-    while (k < n) {  // D^-1
-      if (ip[k] >= 0) {
-        b[k] /= a[k * nb + k];
-        k += 1;
-      } else {
-        const double d11 = a[k * nb + k], d21 = a[(k + 1) * nb + k], d22 = a[(k + 1) * nb + k + 1];
-        const double det = d11 * d22 - d21 * d21;
-        const double b1 = b[k], b2 = b[k + 1];
-        b[k] = (d22 * b1 - d21 * b2) / det;
-        b[k + 1] = (-d21 * b1 + d11 * b2) / det;
-        k += 2;
+    // D^-1 (row operations, independent per column)
+    for (int q = c.lane; q < n; q += c.width) {
+      int kk = 0;
+      while (kk < n) {
+        if (ip[kk] >= 0) {
+          out[kk * nb + q] /= a[kk * nb + kk];
+          kk += 1;
+        } else {
+          const double d11 = a[kk * nb + kk], d21 = a[(kk + 1) * nb + kk], d22 = a[(kk + 1) * nb + kk + 1];
+          const double det = d11 * d22 - d21 * d21;
+          const double b1 = out[kk * nb + q], b2 = out[(kk + 1) * nb + q];
+          out[kk * nb + q] = (d22 * b1 - d21 * b2) / det;
+          out[(kk + 1) * nb + q] = (-d21 * b1 + d11 * b2) / det;
+          kk += 2;
+        }
       }
     }
+    c.sync();
     k = n - 1;
-    while (k >= 0) {  // backward: L^-T then P^T
+    while (k >= 0) {  // L^-T then P^T
       if (ip[k] >= 0) {
-        for (int r = k + 1; r < n; ++r) b[k] -= a[r * nb + k] * b[r];
+        for (int q = c.lane; q < n; q += c.width) {
+          double acc = out[k * nb + q];
+          for (int r = k + 1; r < n; ++r) acc -= a[r * nb + k] * out[r * nb + q];
+          out[k * nb + q] = acc;
+        }
+        c.sync();
         const int kp = ip[k];
-        if (kp != k) { const double t = b[k]; b[k] = b[kp]; b[kp] = t; }
+        if (kp != k) {
+          for (int q = c.lane; q < n; q += c.width) { const double t = out[k * nb + q]; out[k * nb + q] = out[kp * nb + q]; out[kp * nb + q] = t; }
+          c.sync();
+        }
         k -= 1;
       } else {
-        for (int r = k + 1; r < n; ++r) {
-          b[k] -= a[r * nb + k] * b[r];
-          b[k - 1] -= a[r * nb + k - 1] * b[r];
+        for (int q = c.lane; q < n; q += c.width) {
+          double a1 = out[k * nb + q], a0 = out[(k - 1) * nb + q];
+          for (int r = k + 1; r < n; ++r) {
+            a1 -= a[r * nb + k] * out[r * nb + q];
+            a0 -= a[r * nb + k - 1] * out[r * nb + q];
+          }
+          out[k * nb + q] = a1;
+          out[(k - 1) * nb + q] = a0;
         }
+        c.sync();
         const int kp = -ip[k] - 1;
-        if (kp != k) { const double t = b[k]; b[k] = b[kp]; b[kp] = t; }
+        if (kp != k) {
+          for (int q = c.lane; q < n; q += c.width) { const double t = out[k * nb + q]; out[k * nb + q] = out[kp * nb + q]; out[kp * nb + q] = t; }
+          c.sync();
+        }
         k -= 2;
+      }
+    }
+  }
+
+
+  // ---------------------------------------------------------- Riccati path
+  // Stage system with exact dynamics (dc == 0), written on the augmented state
+  // z_i = [x_i, u_{i-1}, tau_{i-1}] and control v_i = [u_i, tau_i] so the jerk
+  // coupling (optimizer.py:461-465) becomes stage-local.  Backward recursion
+  //   Rt = R + B'PB, St = S + B'PA, K = -Rt^-1 St, P <- Q + A'PA + St'K.
+  // The block-tridiagonal KKT system has IPOPT's inertia iff every Rt is
+  // positive definite (Rt are the pivot blocks of the reduced Hessian).
+  // Per-stage storage (slot i of L.LD): P_i [0,64), K_i [64,88).
+  HTP_HD HTP_FI static bool chol3(const double* R, int nv, double* Lc) {  // Lc: 3x3 lower
+    for (int k = 0; k < 9; ++k) Lc[k] = 0.0;
+    for (int j = 0; j < nv; ++j) {
+      double d = R[j * 3 + j];
+      for (int k = 0; k < j; ++k) d -= Lc[j * 3 + k] * Lc[j * 3 + k];
+      if (!(d > 0.0)) return false;
+      d = sqrt(d);
+      Lc[j * 3 + j] = d;
+      for (int r = j + 1; r < nv; ++r) {
+        double v = R[r * 3 + j];
+        for (int k = 0; k < j; ++k) v -= Lc[r * 3 + k] * Lc[j * 3 + k];
+        Lc[r * 3 + j] = v / d;
+      }
+    }
+    return true;
+  }
+  HTP_HD HTP_FI static void chol3_solve(const double* Lc, int nv, double* b) {
+    for (int j = 0; j < nv; ++j) {
+      for (int k = 0; k < j; ++k) b[j] -= Lc[j * 3 + k] * b[k];
+      b[j] /= Lc[j * 3 + j];
+    }
+    for (int j = nv - 1; j >= 0; --j) {
+      for (int k = j + 1; k < nv; ++k) b[j] -= Lc[k * 3 + j] * b[k];
+      b[j] /= Lc[j * 3 + j];
+    }
+  }
+
+  // returns number of stages whose Rt is not positive definite
+  HTP_HD HTP_FI int riccati_factor() {
+    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
+    const gd* scE = A(L.scE);
+    ld* Pc = c.lds;          // 8x8 (stride 8): P_{i+1}
+    ld* Pn = c.lds + 64;     // 8x8: P_i
+    ld* Hw = c.lds + 128;    // 8x8 stage Hessian over w
+    ld* Jm = c.lds + 192;    // 5x8 unscaled dF/dw
+    ld* Cb = c.lds + 232;    // 2x3 jerk cross C_{i-1}
+    ld* PJx = c.lds + 240;   // 8x5
+    ld* PB = c.lds + 280;    // 8x3
+    ld* Rt = c.lds + 304;    // 3x3
+    ld* St = c.lds + 313;    // 3x8
+    ld* AtPA = c.lds + 337;  // 5x5
+    ld* Kl = c.lds + 362;    // 3x8
+    int bad = 0;
+    // stage N-1: P = [[H_xx, 0], [0, 0]]
+    {
+      const gd* Kst = A(L.Kst) + (int64_t)(N - 1) * nb * nb;
+      for (int e = c.lane; e < 64; e += c.width) {
+        const int r = e / 8, q = e % 8;
+        Pc[e] = (r < NS && q < NS) ? Kst[(NS + r) * nb + NS + q] : 0.0;
+      }
+      gd* Ps = A(L.LD) + (int64_t)(N - 1) * nb * nb;
+      c.sync();
+      for (int e = c.lane; e < 64; e += c.width) Ps[e] = Pc[e];
+    }
+    for (int i = N - 2; i >= 0; --i) {
+      // load stage data
+      const gd* Kst = A(L.Kst) + (int64_t)i * nb * nb;
+      const gd* On = A(L.Off) + (int64_t)(i + 1) * nb * nb;
+      const gd* Op = A(L.Off) + (int64_t)i * nb * nb;
+      for (int e = c.lane; e < 64; e += c.width) {
+        const int r = e / 8, q = e % 8;
+        Hw[e] = (r < D.nw && q < D.nw) ? Kst[(NS + r) * nb + NS + q] : 0.0;
+      }
+      for (int e = c.lane; e < 40; e += c.width) {
+        const int k = e / 8, j = e % 8;
+        Jm[e] = (j < D.nw) ? -On[k * nb + NS + j] / scE[D.eDyn + NS * i + k] : 0.0;
+      }
+      for (int e = c.lane; e < 6; e += c.width) {
+        const int a = e / 3, b = e % 3;
+        Cb[e] = (i >= 1 && b < nv) ? Op[(NS + 5 + a) * nb + NS + 5 + b] : 0.0;
+      }
+      c.sync();
+      // PJx = P[:,0:5] Jx ; PB = P[:,0:5] Jv + P[:,5:5+nv]
+      for (int e = c.lane; e < nz * (NS + nv); e += c.width) {
+        const int r = e / (NS + nv), q = e % (NS + nv);
+        double acc = 0.0;
+        for (int t = 0; t < NS; ++t) acc += Pc[r * 8 + t] * Jm[t * 8 + q];
+        if (q < NS) PJx[r * 5 + q] = acc;
+        else PB[r * 3 + (q - NS)] = acc + Pc[r * 8 + NS + (q - NS)];
+      }
+      c.sync();
+      // Rt = R + B'PB ; St = S + B'PA ; AtPA = Jx' P Jx
+      for (int e = c.lane; e < nv * nv + nv * nz + 25; e += c.width) {
+        if (e < nv * nv) {
+          const int a = e / nv, b = e % nv;
+          double acc = Hw[(NS + a) * 8 + NS + b] + PB[(NS + a) * 3 + b];
+          for (int t = 0; t < NS; ++t) acc += Jm[t * 8 + NS + a] * PB[t * 3 + b];
+          Rt[a * 3 + b] = acc;
+        } else if (e < nv * nv + nv * nz) {
+          const int f = e - nv * nv, a = f / nz, q = f % nz;
+          double acc;
+          if (q < NS) {
+            acc = Hw[(NS + a) * 8 + q];
+            for (int t = 0; t < NS; ++t) acc += PB[t * 3 + a] * Jm[t * 8 + q];
+          } else {
+            acc = (a < 2) ? Cb[a * 3 + (q - NS)] : 0.0;
+          }
+          St[a * 8 + q] = acc;
+        } else {
+          const int f = e - nv * nv - nv * nz, r = f / 5, q = f % 5;
+          double acc = 0.0;
+          for (int t = 0; t < NS; ++t) acc += Jm[t * 8 + r] * PJx[t * 5 + q];
+          AtPA[r * 5 + q] = acc;
+        }
+      }
+      c.sync();
+      // Cholesky of Rt (redundantly per lane) ; K = -Rt^-1 St (lane per column)
+      double Rl[9], Lc[9];
+      for (int k = 0; k < 9; ++k) Rl[k] = (k / 3 < nv && k % 3 < nv) ? Rt[k] : 0.0;
+      const bool pd = chol3(Rl, nv, Lc);
+      if (!pd) ++bad;
+      for (int q = c.lane; q < nz; q += c.width) {
+        double col[3] = {0.0, 0.0, 0.0};
+        for (int a = 0; a < nv; ++a) col[a] = St[a * 8 + q];
+        if (pd) chol3_solve(Lc, nv, col);
+        for (int a = 0; a < nv; ++a) Kl[a * 8 + q] = -col[a];
+      }
+      c.sync();
+      // P_i = Q + A'PA + St'K
+      gd* Ps = A(L.LD) + (int64_t)i * nb * nb;
+      for (int e = c.lane; e < 64; e += c.width) {
+        const int r = e / 8, q = e % 8;
+        double acc = 0.0;
+        if (r < nz && q < nz) {
+          if (r < NS && q < NS) acc = Hw[r * 8 + q] + AtPA[r * 5 + q];
+          for (int a = 0; a < nv; ++a) acc += St[a * 8 + r] * Kl[a * 8 + q];
+        }
+        Pn[e] = acc;
+        Ps[e] = acc;
+      }
+      for (int e = c.lane; e < 24; e += c.width) Ps[64 + e] = Kl[e];
+      for (int e = c.lane; e < 9; e += c.width) Ps[88 + e] = Lc[e];
+      c.sync();
+      for (int e = c.lane; e < 64; e += c.width) Pc[e] = 0.5 * (Pn[e] + Pn[(e % 8) * 8 + e / 8]);  // symmetrise
+      c.sync();
+    }
+    return bad;
+  }
+
+  // V (block order [y|x|u|tau]) -> X (same order) with the Riccati factor
+  HTP_HD HTP_FI void riccati_solve(const gd* V, gd* X) {
+    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
+    const gd* scE = A(L.scE);
+    ld* pv = c.lds;          // p_{i+1} (8)
+    ld* wv = c.lds + 8;      // w (8)
+    ld* rt = c.lds + 16;     // rt (3)
+    ld* zv = c.lds + 24;     // z (8)
+    ld* vv = c.lds + 32;     // v (3)
+    // backward: p_{N-1} = [q_{N-1}; 0]
+    {
+      gd* Xl = X + (int64_t)(N - 1) * nb;
+      const gd* Vl = V + (int64_t)(N - 1) * nb;
+      for (int k = c.lane; k < 8; k += c.width) {
+        const double val = (k < NS) ? Vl[NS + k] : 0.0;
+        pv[k] = val;
+        Xl[k] = val;
+      }
+      c.sync();
+    }
+    for (int i = N - 2; i >= 0; --i) {
+      const gd* Pn = A(L.LD) + (int64_t)(i + 1) * nb * nb;  // P_{i+1}
+      const gd* Pi = A(L.LD) + (int64_t)i * nb * nb;        // K_i at +64
+      const gd* On = A(L.Off) + (int64_t)(i + 1) * nb * nb;
+      const gd* Vn = V + (int64_t)(i + 1) * nb;
+      const gd* Vi = V + (int64_t)i * nb;
+      // w = p_{i+1} - P_{i+1}[:, 0:5] e_{i+1}
+      for (int r = c.lane; r < nz; r += c.width) {
+        double acc = pv[r];
+        for (int t = 0; t < NS; ++t) acc -= Pn[r * 8 + t] * (Vn[t] / scE[D.eDyn + NS * i + t]);
+        wv[r] = acc;
+      }
+      c.sync();
+      // rt = r_i + Jv' w[0:5] + w[5:5+nv]
+      for (int a = c.lane; a < nv; a += c.width) {
+        double acc = Vi[NS + NS + a] + wv[NS + a];
+        for (int t = 0; t < NS; ++t) acc += (-On[t * nb + NS + NS + a] / scE[D.eDyn + NS * i + t]) * wv[t];
+        rt[a] = acc;
+      }
+      c.sync();
+      // p_i = q_i + Jx' w[0:5] + K' rt ;  k_i = Rt^-1 rt = -(K... ) -> stored as solve of Rt
+      gd* Xi = X + (int64_t)i * nb;
+      for (int r = c.lane; r < nz; r += c.width) {
+        double acc = (r < NS) ? Vi[NS + r] : 0.0;
+        if (r < NS)
+          for (int t = 0; t < NS; ++t) acc += (-On[t * nb + NS + r] / scE[D.eDyn + NS * i + t]) * wv[t];
+        for (int a = 0; a < nv; ++a) acc += Pi[64 + a * 8 + r] * rt[a];
+        Xi[r] = acc;  // p_i
+      }
+      for (int a = c.lane; a < nv; a += c.width) Xi[nz + a] = rt[a];  // rt_i (k_i = Rt^-1 rt later)
+      c.sync();
+      for (int r = c.lane; r < nz; r += c.width) pv[r] = Xi[r];
+      c.sync();
+    }
+    // forward: z_0 = [x_0; 0], v_i = Rt^-1 rt_i + K_i z_i, y_i = (p_i - P_i z_i)[0:5]
+    ld* pz = c.lds + 40;     // p_i (8)
+    ld* rr = c.lds + 48;     // rt_i (3)
+    ld* yv = c.lds + 56;     // y_i (5)
+    for (int k = c.lane; k < 8; k += c.width) zv[k] = (k < NS) ? V[k] / scE[k] : 0.0;
+    c.sync();
+    for (int i = 0; i < N; ++i) {
+      const gd* Ps = A(L.LD) + (int64_t)i * nb * nb;
+      gd* Xi = X + (int64_t)i * nb;
+      const int ybase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
+      for (int k = c.lane; k < nz; k += c.width) pz[k] = Xi[k];
+      if (i < N - 1)
+        for (int a2 = c.lane; a2 < nv; a2 += c.width) rr[a2] = Xi[nz + a2];
+      c.sync();
+      for (int k = c.lane; k < NS; k += c.width) {
+        double acc = pz[k];
+        for (int t = 0; t < nz; ++t) acc -= Ps[k * 8 + t] * zv[t];
+        yv[k] = acc / scE[ybase + k];
+      }
+      if (i < N - 1) {
+        double kv[3] = {rr[0], nv > 1 ? rr[1] : 0.0, nv > 2 ? rr[2] : 0.0};
+        double Lc[9];
+        for (int e = 0; e < 9; ++e) Lc[e] = Ps[88 + e];
+        chol3_solve(Lc, nv, kv);
+        for (int a2 = c.lane; a2 < nv; a2 += c.width) {
+          double acc = kv[a2];
+          for (int t = 0; t < nz; ++t) acc += Ps[64 + a2 * 8 + t] * zv[t];
+          vv[a2] = acc;
+        }
+      }
+      c.sync();
+      double zn[8];
+      if (i < N - 1) {
+        const gd* On = A(L.Off) + (int64_t)(i + 1) * nb * nb;
+        const gd* Vn = V + (int64_t)(i + 1) * nb;
+        for (int k = c.lane; k < nz; k += c.width) {
+          double acc;
+          if (k < NS) {
+            const double sk = scE[D.eDyn + NS * i + k];
+            acc = Vn[k] / sk;
+            for (int t = 0; t < NS; ++t) acc += (-On[k * nb + NS + t] / sk) * zv[t];
+            for (int a2 = 0; a2 < nv; ++a2) acc += (-On[k * nb + NS + NS + a2] / sk) * vv[a2];
+          } else {
+            acc = vv[k - NS];
+          }
+          zn[(k - c.lane) / c.width] = acc;
+        }
+      }
+      for (int k = c.lane; k < NS; k += c.width) {
+        Xi[k] = yv[k];
+        Xi[NS + k] = zv[k];
+      }
+      if (i < N - 1)
+        for (int a2 = c.lane; a2 < nv; a2 += c.width) Xi[NS + NS + a2] = vv[a2];
+      c.sync();
+      if (i < N - 1) {
+        for (int k = c.lane; k < nz; k += c.width) zv[k] = zn[(k - c.lane) / c.width];
+        c.sync();
       }
     }
   }
 
   // ---------------------------------------------------------- factorization
   // returns true if the inertia is the one IPOPT requires
-  HTP_HD void factorize(bool ls, double dw, double dc, int& neg_out, int& zero_out) {
+  HTP_HD HTP_FI void factorize(bool ls, double dw, double dc, int& neg_out, int& zero_out) {
     const int N = D.N, nb = D.nb;
     int neg = 0, zero = 0;
-    if (uniform44()) local_factor_sweep<4, 4>(ls, dw, dc, neg, zero);
-    else local_factor_sweep<MAXE, MAXE>(ls, dw, dc, neg, zero);
+    long long t0 = c.clock();
+    local_factor_sweep<EN_, EM_>(ls, dw, dc, neg, zero);
     neg = c.isum(neg);
     zero = c.isum(zero);
     c.sync();
+    long long t1 = c.clock();
+    cyc[0] += t1 - t0;
     for (int i = c.lane; i < N; i += c.width) assemble_stage(i, ls, dw, dc);
     c.sync();
-    // sequential block LDL^T over stages, in LDS
-    double* Acur = c.lds;                  // nb x nb
-    double* Dprev = c.lds + NBMAX * NBMAX; // nb x nb
-    double* Ybuf = c.lds + 2 * NBMAX * NBMAX;
-    int* ipp = c.ildsp;                    // pivots of Dprev
-    int* ipc = c.ildsp + NBMAX;
+    long long t2 = c.clock();
+    cyc[1] += t2 - t1;
+    if (dc == 0.0) {
+      const int bad = riccati_factor();
+      use_ric = true;
+      cyc[2] += c.clock() - t2;
+      neg_out = neg + (bad ? -1 : NS * N) + NS + D.md;
+      zero_out = zero;
+      return;
+    }
+    use_ric = false;
+    // sequential block LDL^T over stages, in LDS:
+    //   D_i = K_ii - Off_i Dinv_{i-1} Off_i',  LD_i = Off_i Dinv_{i-1},
+    //   Dinv_i = D_i^{-1} from a Bunch-Kaufman factor (inertia of D_i).
+    ld* Acur = c.lds;                   // nb x nb
+    ld* Dinv = c.lds + NBMAX * NBMAX;   // nb x nb (previous stage inverse)
+    ld* Obuf = c.lds + 2 * NBMAX * NBMAX;
+    ld* Tmp = c.lds + 3 * NBMAX * NBMAX;
+    li* ipc = c.ildsp;
     int sneg = 0, szero = 0;
+    const int nb2 = nb * nb;
     for (int i = 0; i < N; ++i) {
-      const double* K = A(L.Kst) + (int64_t)i * nb * nb;
-      for (int e = c.lane; e < nb * nb; e += c.width) Acur[e] = K[e];
+      const gd* K = A(L.Kst) + (int64_t)i * nb2;
+      for (int e = c.lane; e < nb2; e += c.width) Acur[e] = K[e];
+      if (i > 0) {
+        const gd* O = A(L.Off) + (int64_t)i * nb2;
+        for (int e = c.lane; e < nb2; e += c.width) Obuf[e] = O[e];
+      }
       c.sync();
       if (i > 0) {
-        const double* O = A(L.Off) + (int64_t)i * nb * nb;
-        // Y(:, j) = Dprev^-1 O(j, :)'   (lane j)
-        for (int j = c.lane; j < nb; j += c.width) {
-          double v[NBMAX];
-          for (int r = 0; r < nb; ++r) v[r] = O[j * nb + r];
-          bk_solve_serial(Dprev, ipp, nb, v);
-          for (int r = 0; r < nb; ++r) Ybuf[r * nb + j] = v[r];
-        }
-        c.sync();
-        // LD = O Dprev^-1 = Y' ; Acur -= O Y
-        double* LD = A(L.LD) + (int64_t)i * nb * nb;
-        for (int e = c.lane; e < nb * nb; e += c.width) {
+        gd* LD = A(L.LD) + (int64_t)i * nb2;
+        for (int e = c.lane; e < nb2; e += c.width) {  // Tmp = LD = Off Dinv
           const int r = e / nb, q = e % nb;
           double acc = 0.0;
-          for (int t = 0; t < nb; ++t) acc += O[r * nb + t] * Ybuf[t * nb + q];
+          for (int t = 0; t < nb; ++t) acc += Obuf[r * nb + t] * Dinv[t * nb + q];
+          Tmp[e] = acc;
+          LD[e] = acc;
+        }
+        c.sync();
+        for (int e = c.lane; e < nb2; e += c.width) {  // Acur -= LD Off'
+          const int r = e / nb, q = e % nb;
+          double acc = 0.0;
+          for (int t = 0; t < nb; ++t) acc += Tmp[r * nb + t] * Obuf[q * nb + t];
           Acur[e] -= acc;
-          LD[e] = Ybuf[q * nb + r];
         }
         c.sync();
       }
       bk_factor(Acur, ipc, nb, sneg, szero);
-      double* F = A(L.fac) + (int64_t)i * nb * nb;
-      double* IP = A(L.ipiv) + (int64_t)i * nb;
-      for (int e = c.lane; e < nb * nb; e += c.width) {
-        F[e] = Acur[e];
-        Dprev[e] = Acur[e];
-      }
-      for (int e = c.lane; e < nb; e += c.width) {
-        IP[e] = ipc[e];
-        ipp[e] = ipc[e];
-      }
+      bk_inverse(Acur, ipc, nb, Dinv);
+      gd* F = A(L.fac) + (int64_t)i * nb2;
+      for (int e = c.lane; e < nb2; e += c.width) F[e] = Dinv[e];
       c.sync();
     }
+    cyc[2] += c.clock() - t2;
     // terminal block contributes 5 negatives; inequality multipliers md negatives
 #ifdef HTP_HOST_DEBUG
     printf("[dbg]   pairs neg=%d (exp %d) zero=%d stages neg=%d (exp %d) zero=%d\n", neg, 2 * D.P, zero, sneg, NS * N, szero);
@@ -1113,20 +1451,19 @@ struct ObcaSolver {
   }
 
   // solve K [ox; os; oc; od] = [bx; bs; bc; bd] with the current factorization
-  HTP_HD void kkt_solve(bool ls, double dw, double dc, const double* bx, const double* bs, const double* bc,
-                        const double* bd, double* ox, double* os, double* oc, double* od) {
+  HTP_HD HTP_FI void kkt_solve(bool ls, double dw, double dc, const gd* bx, const gd* bs, const gd* bc,
+                        const gd* bd, gd* ox, gd* os, gd* oc, gd* od) {
     const int N = D.N, nb = D.nb;
-    const bool u44 = uniform44();
-    if (u44) local_rhs_sweep<4, 4>(ls, dw, dc, bx, bs, bc, bd);
-    else local_rhs_sweep<MAXE, MAXE>(ls, dw, dc, bx, bs, bc, bd);
+    const long long t0 = c.clock();
+    local_rhs_sweep<EN_, EM_>(ls, dw, dc, bx, bs, bc, bd);
     c.sync();
-    const double* PR = A(L.pairR);
-    const double* scE = A(L.scE);
-    double* V = A(L.V);
+    const gd* PR = A(L.pairR);
+    const gd* scE = A(L.scE);
+    gd* V = A(L.V);
     const int MK = D.M * D.K;
     const double Hs = ls ? 1.0 : 10000.0 * sf + dw;
     for (int i = c.lane; i < N; i += c.width) {
-      double* r = V + (int64_t)i * nb;
+      gd* r = V + (int64_t)i * nb;
       const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
       for (int k = 0; k < NS; ++k) r[k] = bc[rowbase + k];
       for (int k = 0; k < NS; ++k) r[NS + k] = bx[NS * i + k];
@@ -1150,11 +1487,15 @@ struct ObcaSolver {
       }
     }
     c.sync();
+    gd* X = A(L.X);
+    if (use_ric) {
+      riccati_solve(V, X);
+    } else {
     // forward: V_i -= LD_i V_{i-1}
     for (int i = 1; i < N; ++i) {
-      const double* LD = A(L.LD) + (int64_t)i * nb * nb;
-      double* vi = V + (int64_t)i * nb;
-      const double* vp = V + (int64_t)(i - 1) * nb;
+      const gd* LD = A(L.LD) + (int64_t)i * nb * nb;
+      gd* vi = V + (int64_t)i * nb;
+      const gd* vp = V + (int64_t)(i - 1) * nb;
       for (int r = c.lane; r < nb; r += c.width) {
         double acc = 0.0;
         for (int t = 0; t < nb; ++t) acc += LD[r * nb + t] * vp[t];
@@ -1162,33 +1503,33 @@ struct ObcaSolver {
       }
       c.sync();
     }
-    // backward
-    double* X = A(L.X);
+    // backward: X_i = Dinv_i (V_i - Off_{i+1}' X_{i+1})
+    ld* tv = c.lds + 3 * NBMAX * NBMAX;
     for (int i = N - 1; i >= 0; --i) {
-      double* xi = X + (int64_t)i * nb;
-      const double* vi = V + (int64_t)i * nb;
+      gd* xi = X + (int64_t)i * nb;
+      const gd* vi = V + (int64_t)i * nb;
       for (int r = c.lane; r < nb; r += c.width) {
         double acc = vi[r];
         if (i < N - 1) {
-          const double* O = A(L.Off) + (int64_t)(i + 1) * nb * nb;
-          const double* xn = X + (int64_t)(i + 1) * nb;
+          const gd* O = A(L.Off) + (int64_t)(i + 1) * nb * nb;
+          const gd* xn = X + (int64_t)(i + 1) * nb;
           for (int t = 0; t < nb; ++t) acc -= O[t * nb + r] * xn[t];
         }
+        tv[r] = acc;
+      }
+      c.sync();
+      const gd* F = A(L.fac) + (int64_t)i * nb * nb;
+      for (int r = c.lane; r < nb; r += c.width) {
+        double acc = 0.0;
+        for (int t = 0; t < nb; ++t) acc += F[r * nb + t] * tv[t];
         xi[r] = acc;
       }
       c.sync();
-      if (c.lane == 0) {
-        const double* F = A(L.fac) + (int64_t)i * nb * nb;
-        const double* IPd = A(L.ipiv) + (int64_t)i * nb;
-        int ipv[NBMAX];
-        for (int t = 0; t < nb; ++t) ipv[t] = (int)IPd[t];
-        bk_solve_serial(F, ipv, nb, xi);
-      }
-      c.sync();
+    }
     }
     // scatter stage solution
     for (int i = c.lane; i < N; i += c.width) {
-      const double* xi = X + (int64_t)i * nb;
+      const gd* xi = X + (int64_t)i * nb;
       const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
       for (int k = 0; k < NS; ++k) oc[rowbase + k] = xi[k];
       for (int k = 0; k < NS; ++k) ox[NS * i + k] = xi[NS + k];
@@ -1207,18 +1548,18 @@ struct ObcaSolver {
       }
     }
     c.sync();
-    if (u44) local_back_sweep<4, 4>(ls, dw, dc, bx, bs, bc, bd, ox, os, oc, od);
-    else local_back_sweep<MAXE, MAXE>(ls, dw, dc, bx, bs, bc, bd, ox, os, oc, od);
+    local_back_sweep<EN_, EM_>(ls, dw, dc, bx, bs, bc, bd, ox, os, oc, od);
     c.sync();
+    cyc[3] += c.clock() - t0;
   }
   // ======================================================== IPM driver
   // Mirrors oracle/ipm.py IpoptRestatement.solve line by line.
   int nbL, nbU, nsL, nsU;  // counts of finite bounds
 
-  HTP_HD void count_bounds() {
-    const double* xL = A(L.xL);
-    const double* xU = A(L.xU);
-    const double* dU = A(L.dU);
+  HTP_HD HTP_FI void count_bounds() {
+    const gd* xL = A(L.xL);
+    const gd* xU = A(L.xU);
+    const gd* dU = A(L.dU);
     int a = 0, b = 0, e = 0;
     for (int q = c.lane; q < D.n; q += c.width) {
       a += finite_(xL[q]);
@@ -1234,20 +1575,20 @@ struct ObcaSolver {
   struct Err { double dual, comp, s_d, s_c, prim_b, prim_nlp; };
 
   // grad Lagrangian (x part, w/o bound multipliers) -> rx
-  HTP_HD void grad_lag_into(double* out) {
+  HTP_HD HTP_FI void grad_lag_into(gd* out) {
     eval_jt(A(L.x), A(L.yc), A(L.yd), out);
-    const double* gf = A(L.gf);
+    const gd* gf = A(L.gf);
     for (int q = c.lane; q < D.n; q += c.width) out[q] += gf[q];
     c.sync();
   }
 
-  HTP_HD Err errors(const double* gl, double mu_) const {
-    const double* x = A(L.x); const double* xL = A(L.xL); const double* xU = A(L.xU);
-    const double* zL = A(L.zL); const double* zU = A(L.zU);
-    const double* s = A(L.s); const double* dL = A(L.dL); const double* dU = A(L.dU);
-    const double* vL = A(L.vL); const double* vU = A(L.vU);
-    const double* yc = A(L.yc); const double* yd = A(L.yd);
-    const double* cc = A(L.c); const double* dd = A(L.d);
+  HTP_HD HTP_FI Err errors(const gd* gl, double mu_) const {
+    const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
+    const gd* zL = A(L.zL); const gd* zU = A(L.zU);
+    const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
+    const gd* vL = A(L.vL); const gd* vU = A(L.vU);
+    const gd* yc = A(L.yc); const gd* yd = A(L.yd);
+    const gd* cc = A(L.c); const gd* dd = A(L.d);
     double dual = 0, comp = 0, zsum = 0, ysum = 0, pb = 0, pn = 0;
     for (int q = c.lane; q < D.n; q += c.width) {
       dual = dmax(dual, dabs(gl[q] - zL[q] + zU[q]));
@@ -1284,9 +1625,9 @@ struct ObcaSolver {
   }
 
   // unscaled constraint violation of the original NLP at x (uses c, d arrays)
-  HTP_HD double unscaled_viol() const {
-    const double* cc = A(L.c); const double* dd = A(L.d);
-    const double* scE = A(L.scE); const double* scI = A(L.scI);
+  HTP_HD HTP_FI double unscaled_viol() const {
+    const gd* cc = A(L.c); const gd* dd = A(L.d);
+    const gd* scE = A(L.scE); const gd* scI = A(L.scI);
     const double dmn = par(P_DMIN);
     double v = 0;
     for (int r = c.lane; r < D.mc; r += c.width) v = dmax(v, dabs(cc[r]) / scE[r]);
@@ -1298,7 +1639,7 @@ struct ObcaSolver {
     return c.maxv(v);
   }
 
-  HTP_HD double theta_of(const double* cc, const double* dd, const double* s) const {
+  HTP_HD HTP_FI double theta_of(const gd* cc, const gd* dd, const gd* s) const {
     double t = 0;
     for (int r = c.lane; r < D.mc; r += c.width) t += dabs(cc[r]);
     for (int r = c.lane; r < D.md; r += c.width) t += dabs(dd[r] - s[r]);
@@ -1306,9 +1647,9 @@ struct ObcaSolver {
   }
 
   // barrier function; returns +inf (as 1e308*10) if a slack is not positive
-  HTP_HD double barrier(const double* x, const double* s, double mu_) const {
-    const double* xL = A(L.xL); const double* xU = A(L.xU);
-    const double* dL = A(L.dL); const double* dU = A(L.dU);
+  HTP_HD HTP_FI double barrier(const gd* x, const gd* s, double mu_) const {
+    const gd* xL = A(L.xL); const gd* xU = A(L.xU);
+    const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     const double kd = o.kappa_d * mu_;
     double lg = 0.0, lin = 0.0;
     int bad = 0;
@@ -1332,10 +1673,10 @@ struct ObcaSolver {
   }
 
   // barrier gradient -> gx (n), gs (md); needs gf current
-  HTP_HD void grad_barrier(double mu_, double* gx, double* gs) const {
-    const double* x = A(L.x); const double* xL = A(L.xL); const double* xU = A(L.xU);
-    const double* s = A(L.s); const double* dL = A(L.dL); const double* dU = A(L.dU);
-    const double* gf = A(L.gf);
+  HTP_HD HTP_FI void grad_barrier(double mu_, gd* gx, gd* gs) const {
+    const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
+    const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
+    const gd* gf = A(L.gf);
     const double kd = o.kappa_d * mu_;
     for (int q = c.lane; q < D.n; q += c.width) {
       const bool hl = finite_(xL[q]), hu = finite_(xU[q]);
@@ -1356,9 +1697,9 @@ struct ObcaSolver {
     c.sync();
   }
 
-  HTP_HD double frac_primal(const double* dx, const double* ds) const {
-    const double* x = A(L.x); const double* xL = A(L.xL); const double* xU = A(L.xU);
-    const double* s = A(L.s); const double* dL = A(L.dL); const double* dU = A(L.dU);
+  HTP_HD HTP_FI double frac_primal(const gd* dx, const gd* ds) const {
+    const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
+    const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     double a = 1.0;
     for (int q = c.lane; q < D.n; q += c.width) {
       if (finite_(xL[q]) && dx[q] < 0) a = dmin(a, -tau * (x[q] - xL[q]) / dx[q]);
@@ -1372,12 +1713,12 @@ struct ObcaSolver {
   }
 
   // bound-multiplier steps for (dx, ds) -> dzL, dzU, dvL, dvU ; returns alpha_dual
-  HTP_HD double dual_steps(const double* dx, const double* ds) {
-    const double* x = A(L.x); const double* xL = A(L.xL); const double* xU = A(L.xU);
-    const double* s = A(L.s); const double* dL = A(L.dL); const double* dU = A(L.dU);
-    const double* zL = A(L.zL); const double* zU = A(L.zU);
-    const double* vL = A(L.vL); const double* vU = A(L.vU);
-    double* dzL = A(L.dzL); double* dzU = A(L.dzU); double* dvL = A(L.dvL); double* dvU = A(L.dvU);
+  HTP_HD HTP_FI double dual_steps(const gd* dx, const gd* ds) {
+    const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
+    const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
+    const gd* zL = A(L.zL); const gd* zU = A(L.zU);
+    const gd* vL = A(L.vL); const gd* vU = A(L.vU);
+    gd* dzL = A(L.dzL); gd* dzU = A(L.dzU); gd* dvL = A(L.dvL); gd* dvU = A(L.dvU);
     double a = 1.0;
     for (int q = c.lane; q < D.n; q += c.width) {
       double t = 0.0, u = 0.0;
@@ -1399,12 +1740,12 @@ struct ObcaSolver {
     return c.minv(a);
   }
 
-  HTP_HD static bool cmp_le(double lhs, double rhs, double basval) {
+  HTP_HD HTP_FI static bool cmp_le(double lhs, double rhs, double basval) {
     return lhs - rhs <= 10.0 * 2.220446049250313e-16 * dabs(basval);
   }
 
   // factorization with inertia correction (IPOPT PDPerturbationHandler, simplified)
-  HTP_HD bool factor_ic(double& dw, double& dc) {
+  HTP_HD HTP_FI bool factor_ic(double& dw, double& dc) {
     dw = 0.0;
     dc = 0.0;
     const int need = D.mc + D.md;
@@ -1424,10 +1765,10 @@ struct ObcaSolver {
   }
 
   // trial acceptability test (filter / Armijo); evaluates ct, dt at (xt, st)
-  HTP_HD bool acceptable(double a, const double* xt, const double* st, double phi, double theta, double gBD,
+  HTP_HD HTP_FI bool acceptable(double a, const gd* xt, const gd* st, double phi, double theta, double gBD,
                          bool ftype_ok, double& th_t, double& ph_t) {
-    double* ct = A(L.ct);
-    double* dtv = A(L.dt);
+    gd* ct = A(L.ct);
+    gd* dtv = A(L.dt);
     eval_cons(xt, ct, dtv);
     th_t = theta_of(ct, dtv, st);
     ph_t = barrier(xt, st, mu);
@@ -1441,26 +1782,38 @@ struct ObcaSolver {
     return true;
   }
 
-  HTP_HD void run(Result& res) {
+  HTP_HD HTP_FI void run(Result& res) {
+    for (int k = 0; k < 6; ++k) cyc[k] = 0;
+    const long long t0 = c.clock();
     initialize();
     iterate(res);
+    if (c.lane == 0) {
+      for (int k = 0; k < 6; ++k) res.cyc[k] = cyc[k];
+      res.cyc[4] = c.clock() - t0;
+    }
   }
 
-  HTP_HD void initialize() {
+  HTP_HD HTP_FI void initialize() {
     n_factor = 0;
+    for (int k = 0; k < 6; ++k) cyc[k] = 0;
     dw_last = 0.0;
     nfilt = 0;
     set_bounds_and_x0();
+    HTP_TRACE("[trace] bounds\n");
     compute_scaling();
+    HTP_TRACE("[trace] scaling sf=%g\n", sf);
     relax_and_push();
-    double* x = A(L.x); double* s = A(L.s);
-    double* cc = A(L.c); double* dd = A(L.d);
+    HTP_TRACE("[trace] push\n");
+    gd* x = A(L.x); gd* s = A(L.s);
+    gd* cc = A(L.c); gd* dd = A(L.d);
     eval_cons(x, cc, dd);
+    HTP_TRACE("[trace] cons\n");
     set_slack_bounds_and_push();
     count_bounds();
+    HTP_TRACE("[trace] counted %d %d %d\n", nbL, nbU, nsU);
     {
-      const double* xL = A(L.xL); const double* xU = A(L.xU); const double* dU = A(L.dU);
-      double* zL = A(L.zL); double* zU = A(L.zU); double* vL = A(L.vL); double* vU = A(L.vU);
+      const gd* xL = A(L.xL); const gd* xU = A(L.xU); const gd* dU = A(L.dU);
+      gd* zL = A(L.zL); gd* zU = A(L.zU); gd* vL = A(L.vL); gd* vU = A(L.vU);
       for (int q = c.lane; q < D.n; q += c.width) {
         zL[q] = finite_(xL[q]) ? o.bound_mult_init_val : 0.0;
         zU[q] = finite_(xU[q]) ? o.bound_mult_init_val : 0.0;
@@ -1469,7 +1822,7 @@ struct ObcaSolver {
         vL[r] = o.bound_mult_init_val;
         vU[r] = finite_(dU[r]) ? o.bound_mult_init_val : 0.0;
       }
-      double* yc = A(L.yc); double* yd = A(L.yd);
+      gd* yc = A(L.yc); gd* yd = A(L.yd);
       for (int r = c.lane; r < D.mc; r += c.width) yc[r] = 0.0;
       for (int r = c.lane; r < D.md; r += c.width) yd[r] = 0.0;
       c.sync();
@@ -1480,25 +1833,27 @@ struct ObcaSolver {
       int neg, zero;
       factorize(true, 0.0, 0.0, neg, zero);
       ++n_factor;
+      HTP_TRACE("[trace] LS factor neg=%d zero=%d\n", neg, zero);
 #ifdef HTP_HOST_DEBUG
       printf("[dbg] LS factor neg=%d need=%d zero=%d\n", neg, D.mc + D.md, zero);
 #endif
       if (neg == D.mc + D.md && zero == 0) {
-        double* bx = A(L.rx); double* bs = A(L.rs); double* bc = A(L.rc); double* bd = A(L.rd);
-        const double* gf = A(L.gf);
-        const double* zL = A(L.zL); const double* zU = A(L.zU); const double* vL = A(L.vL); const double* vU = A(L.vU);
+        gd* bx = A(L.rx); gd* bs = A(L.rs); gd* bc = A(L.rc); gd* bd = A(L.rd);
+        const gd* gf = A(L.gf);
+        const gd* zL = A(L.zL); const gd* zU = A(L.zU); const gd* vL = A(L.vL); const gd* vU = A(L.vU);
         for (int q = c.lane; q < D.n; q += c.width) bx[q] = -(gf[q] - zL[q] + zU[q]);
         for (int r = c.lane; r < D.md; r += c.width) { bs[r] = -(-vL[r] + vU[r]); bd[r] = 0.0; }
         for (int r = c.lane; r < D.mc; r += c.width) bc[r] = 0.0;
         c.sync();
         kkt_solve(true, 0.0, 0.0, bx, bs, bc, bd, A(L.dx), A(L.ds), A(L.dyc), A(L.dyd));
-        const double* a1 = A(L.dyc); const double* a2 = A(L.dyd);
+        HTP_TRACE("[trace] LS solve\n");
+        const gd* a1 = A(L.dyc); const gd* a2 = A(L.dyd);
         double mx = 0.0;
         for (int r = c.lane; r < D.mc; r += c.width) mx = dmax(mx, dabs(a1[r]));
         for (int r = c.lane; r < D.md; r += c.width) mx = dmax(mx, dabs(a2[r]));
         mx = c.maxv(mx);
         if (mx <= o.constr_mult_init_max) {
-          double* yc = A(L.yc); double* yd = A(L.yd);
+          gd* yc = A(L.yc); gd* yd = A(L.yd);
           for (int r = c.lane; r < D.mc; r += c.width) yc[r] = a1[r];
           for (int r = c.lane; r < D.md; r += c.width) yd[r] = a2[r];
         }
@@ -1514,15 +1869,16 @@ struct ObcaSolver {
     }
   }
 
-  HTP_HD void iterate(Result& res) {
-    double* x = A(L.x); double* s = A(L.s);
-    double* cc = A(L.c); double* dd = A(L.d);
+  HTP_HD HTP_FI void iterate(Result& res) {
+    gd* x = A(L.x); gd* s = A(L.s);
+    gd* cc = A(L.c); gd* dd = A(L.d);
     int status = ST_MAXITER, it = 0, acc_count = 0;
     double nlp_err = 0.0;
-    double* gl = A(L.rx);
+    gd* gl = A(L.rx);
     for (it = 0; it <= o.max_iter; ++it) {
       grad_lag_into(gl);
       Err e0 = errors(gl, 0.0);
+      HTP_TRACE("[trace] it %d err dual=%g comp=%g prim=%g mu=%g\n", it, e0.dual, e0.comp, e0.prim_nlp, mu);
       nlp_err = dmax(dmax(e0.dual / e0.s_d, e0.prim_nlp), e0.comp / e0.s_c);
       const double uv = unscaled_viol();
       if (nlp_err <= o.tol && e0.dual / sf <= o.dual_inf_tol && uv <= o.constr_viol_tol && e0.comp / sf <= o.compl_inf_tol) {
@@ -1548,14 +1904,14 @@ struct ObcaSolver {
         nfilt = 0;
       }
       // Newton rhs: rx = grad_barrier + J'y ; rs = gbs - yd ; rc = c ; rd = d - s  (negated below)
-      double* gbx = A(L.sx);   // scratch for barrier gradient
-      double* gbs = A(L.ss);
+      gd* gbx = A(L.sx);   // scratch for barrier gradient
+      gd* gbs = A(L.ss);
       grad_barrier(mu, gbx, gbs);
-      double* rx = A(L.xt);    // use xt as rhs storage (x part), rebuilt below
-      double* rs = A(L.rs); double* rc = A(L.rc); double* rd = A(L.rd);
+      gd* rx = A(L.xt);    // use xt as rhs storage (x part), rebuilt below
+      gd* rs = A(L.rs); gd* rc = A(L.rc); gd* rd = A(L.rd);
       {
-        const double* gf = A(L.gf);
-        const double* yd = A(L.yd);
+        const gd* gf = A(L.gf);
+        const gd* yd = A(L.yd);
         for (int q = c.lane; q < D.n; q += c.width) rx[q] = -(gl[q] - gf[q] + gbx[q]);
         for (int r = c.lane; r < D.md; r += c.width) { rs[r] = -(gbs[r] - yd[r]); rd[r] = -(dd[r] - s[r]); }
         for (int r = c.lane; r < D.mc; r += c.width) rc[r] = -cc[r];
@@ -1564,8 +1920,10 @@ struct ObcaSolver {
       double dw, dc;
       if (!factor_ic(dw, dc)) { status = ST_STEPFAIL; break; }
       if (dw > 0.0) dw_last = dw;
-      double* dx = A(L.dx); double* ds = A(L.ds); double* dyc = A(L.dyc); double* dyd = A(L.dyd);
+      gd* dx = A(L.dx); gd* ds = A(L.ds); gd* dyc = A(L.dyc); gd* dyd = A(L.dyd);
+      HTP_TRACE("[trace] factored dw=%g\n", dw);
       kkt_solve(false, dw, dc, rx, rs, rc, rd, dx, ds, dyc, dyd);
+      HTP_TRACE("[trace] solved\n");
       // line search
       const double phi = barrier(x, s, mu);
       const double theta = theta_of(cc, dd, s);
@@ -1582,10 +1940,10 @@ struct ObcaSolver {
       a_min *= o.alpha_min_frac;
       auto is_ftype = [&](double a) { return gBD < 0 && a * pow(-gBD, o.s_phi) > o.delta * pow(theta, o.s_theta); };
       // keep the Newton rhs (x part) for SOC solves: copy into sx after gbx is consumed
-      double* rxk = A(L.sx);
+      gd* rxk = A(L.sx);
       for (int q = c.lane; q < D.n; q += c.width) rxk[q] = rx[q];
       c.sync();
-      double* xt = A(L.xt); double* st = A(L.st);
+      gd* xt = A(L.xt); gd* st = A(L.st);
       double alpha = alpha_max, a_primal = alpha, a_test = alpha, th_t = 0, ph_t = 0;
       bool accepted = false, soc_used = false, first = true;
       while (alpha >= a_min) {
@@ -1597,15 +1955,15 @@ struct ObcaSolver {
           break;
         }
         if (first && th_t >= theta && o.max_soc > 0) {
-          double* csoc = A(L.csoc); double* dsoc = A(L.dsoc);
-          const double* ct = A(L.ct); const double* dtv = A(L.dt);
+          gd* csoc = A(L.csoc); gd* dsoc = A(L.dsoc);
+          const gd* ct = A(L.ct); const gd* dtv = A(L.dt);
           for (int r = c.lane; r < D.mc; r += c.width) csoc[r] = alpha * cc[r] + ct[r];
           for (int r = c.lane; r < D.md; r += c.width) dsoc[r] = alpha * (dd[r] - s[r]) + (dtv[r] - st[r]);
           c.sync();
           double th_old = theta;
-          double* sx = A(L.dzL);  // temporaries (dz arrays are recomputed after acceptance)
-          double* ss_ = A(L.dvL); double* syc = A(L.syc); double* syd = A(L.syd);
-          double* nrc = A(L.ct); double* nrd = A(L.dt);
+          gd* sx = A(L.dzL);  // temporaries (dz arrays are recomputed after acceptance)
+          gd* ss_ = A(L.dvL); gd* syc = A(L.syc); gd* syd = A(L.syd);
+          gd* nrc = A(L.ct); gd* nrd = A(L.dt);
           for (int k = 0; k < o.max_soc; ++k) {
             for (int r = c.lane; r < D.mc; r += c.width) nrc[r] = -csoc[r];
             for (int r = c.lane; r < D.md; r += c.width) nrd[r] = -dsoc[r];
@@ -1626,7 +1984,7 @@ struct ObcaSolver {
             }
             if (th_soc > o.kappa_soc * th_old) break;
             th_old = th_soc;
-            const double* ct2 = A(L.ct); const double* dt2 = A(L.dt);
+            const gd* ct2 = A(L.ct); const gd* dt2 = A(L.dt);
             for (int r = c.lane; r < D.mc; r += c.width) csoc[r] = a_soc * csoc[r] + ct2[r];
             for (int r = c.lane; r < D.md; r += c.width) dsoc[r] = a_soc * dsoc[r] + (dt2[r] - st[r]);
             c.sync();
@@ -1640,18 +1998,23 @@ struct ObcaSolver {
       (void)soc_used;
       // filter augmentation (uses the accepted trial's barrier value)
       if (!(is_ftype(a_test) && cmp_le(ph_t - phi, o.eta_phi * a_test * gBD, phi))) {
-        if (nfilt < FMAX) { f_th[nfilt] = (1 - o.gamma_theta) * theta; f_ph[nfilt] = phi - o.gamma_phi * theta; ++nfilt; }
-        else { for (int k = 1; k < FMAX; ++k) { f_th[k - 1] = f_th[k]; f_ph[k - 1] = f_ph[k]; }
-               f_th[FMAX - 1] = (1 - o.gamma_theta) * theta; f_ph[FMAX - 1] = phi - o.gamma_phi * theta; }
+        c.sync();
+        if (c.lane == 0) {
+          if (nfilt < FMAX) { f_th[nfilt] = (1 - o.gamma_theta) * theta; f_ph[nfilt] = phi - o.gamma_phi * theta; }
+          else { for (int k = 1; k < FMAX; ++k) { f_th[k - 1] = f_th[k]; f_ph[k - 1] = f_ph[k]; }
+                 f_th[FMAX - 1] = (1 - o.gamma_theta) * theta; f_ph[FMAX - 1] = phi - o.gamma_phi * theta; }
+        }
+        if (nfilt < FMAX) ++nfilt;
+        c.sync();
       }
       const double a_dual = dual_steps(dx, ds);
       {
-        double* zL = A(L.zL); double* zU = A(L.zU); double* vL = A(L.vL); double* vU = A(L.vU);
-        double* yc = A(L.yc); double* yd = A(L.yd);
-        const double* dzL = A(L.dzL); const double* dzU = A(L.dzU);
-        const double* dvL = A(L.dvL); const double* dvU = A(L.dvU);
-        const double* xL = A(L.xL); const double* xU = A(L.xU);
-        const double* dL = A(L.dL); const double* dU = A(L.dU);
+        gd* zL = A(L.zL); gd* zU = A(L.zU); gd* vL = A(L.vL); gd* vU = A(L.vU);
+        gd* yc = A(L.yc); gd* yd = A(L.yd);
+        const gd* dzL = A(L.dzL); const gd* dzU = A(L.dzU);
+        const gd* dvL = A(L.dvL); const gd* dvU = A(L.dvU);
+        const gd* xL = A(L.xL); const gd* xU = A(L.xU);
+        const gd* dL = A(L.dL); const gd* dU = A(L.dU);
         const double ks = o.kappa_sigma;
         for (int q = c.lane; q < D.n; q += c.width) {
           x[q] += a_primal * dx[q];
@@ -1686,8 +2049,8 @@ struct ObcaSolver {
   }
 
   // recompute original (unrelaxed) bounds and clip x
-  HTP_HD void project_original_bounds() {
-    double* x = A(L.x);
+  HTP_HD HTP_FI void project_original_bounds() {
+    gd* x = A(L.x);
     const double vmax = dabs(par(P_MAXV)), smax = dabs(par(P_MAXSTEER));
     const double amax = dabs(par(P_MAXACC)), wmax = dabs(par(P_MAXSR));
     const double twopi = 2.0 * M_PI;

@@ -8,10 +8,15 @@ namespace htp {
 
 #if defined(__HIPCC__)
 struct DevWave {
+  using gd = __attribute__((address_space(1))) double;  // HBM (global) doubles
+  using ld = __attribute__((address_space(3))) double;  // LDS doubles
+  using li = __attribute__((address_space(3))) int;     // LDS ints
+  template <class T>
+  using cst = const __attribute__((address_space(4))) T;  // constant (scalar-cached) memory
   static constexpr int width = 64;
   int lane;
-  double* lds;  // per-wave LDS scratch
-  int* ildsp;   // per-wave LDS int scratch
+  ld* lds;    // per-wave LDS scratch
+  li* ildsp;  // per-wave LDS int scratch
   __device__ __forceinline__ void sync() const { __syncthreads(); }
   __device__ __forceinline__ double sum(double v) const {
 #pragma unroll
@@ -34,10 +39,16 @@ struct DevWave {
     return v;
   }
   __device__ __forceinline__ double bcast(double v, int src) const { return __shfl(v, src, 64); }
+  __device__ __forceinline__ long long clock() const { return (long long)__builtin_amdgcn_s_memtime(); }
 };
 #endif
 
 struct HostLane {
+  using gd = double;
+  using ld = double;
+  using li = int;
+  template <class T>
+  using cst = const T;
   static constexpr int width = 1;
   int lane = 0;
   double* lds;
@@ -48,6 +59,7 @@ struct HostLane {
   double minv(double v) const { return v; }
   int isum(int v) const { return v; }
   double bcast(double v, int) const { return v; }
+  long long clock() const { return 0; }
 };
 
 }  // namespace htp

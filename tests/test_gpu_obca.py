@@ -1,0 +1,67 @@
+"""GPU parity: the HIP solver (libhtp.so via the C ABI) against the oracle.
+
+* small shapes: state trajectories vs the dense IPOPT restatement (oracle/ipm.py)
+  within 1e-4 (north_star tolerance), identical solver status;
+* full config shapes: size-independent properties -- KKT conditions of the
+  oracle NLP at the returned point, batch-composition invariance and
+  determinism.
+"""
+import numpy as np
+import pytest
+
+from headland_trajectory_planning_amd import _native, synth
+from oracle.ipm import IpoptRestatement
+from oracle.nlp import ObcaNLP
+
+pytestmark = pytest.mark.gpu
+
+STATE_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return _native.Context(0)
+
+
+@pytest.mark.parametrize("N,M,imp,topt", [(12, 2, "mower", True), (10, 3, "none", True), (12, 2, "none", False),
+                                          (8, 1, "pruner", True)])
+def test_parity_small_vs_oracle(ctx, N, M, imp, topt):
+    W = np.diag([10.0, 0.1 if topt else 0.0])
+    insts = [synth.make_instance(pid, N=N, M=M, implement=imp, W=W) for pid in range(3)]
+    res = ctx.solve(_native.PackedBatch(insts))
+    for k, inst in enumerate(insts):
+        nlp = ObcaNLP(inst)
+        ref = IpoptRestatement(nlp).solve()
+        assert res.status[k] == ref["status"]
+        xs, rs = res.x[k, :5 * N], ref["x"][:5 * N]
+        assert np.max(np.abs(xs - rs)) <= STATE_TOL
+        assert abs(res.objective[k] - ref["f"]) <= 1e-6 * max(1.0, abs(ref["f"]))
+
+
+def _kkt_residuals(nlp, x):
+    """Primal feasibility of the oracle NLP at x (size independent)."""
+    g = nlp.cons(x)
+    viol = np.maximum(0, np.maximum(nlp.g_L - g, g - nlp.g_U))
+    viol[nlp.g_L == nlp.g_U] = np.abs(g - nlp.g_L)[nlp.g_L == nlp.g_U]
+    bnd = np.maximum(0, np.maximum(nlp.x_L - x, x - nlp.x_U))
+    return viol.max(), bnd.max()
+
+
+@pytest.mark.parametrize("cfg", ["B", "C"])
+def test_full_config_properties(ctx, cfg):
+    _, N, M, imp = synth.CONFIGS[cfg]
+    insts = [synth.make_instance(pid, N=N, M=M, implement=imp) for pid in range(64)]
+    pk = _native.PackedBatch(insts)
+    res = ctx.solve(pk)
+    ok = np.isin(res.status, [0, 1])
+    assert ok.mean() >= 0.9, np.bincount(res.status)
+    for k in np.where(ok)[0][:8]:
+        nlp = ObcaNLP(insts[k])
+        cv, bv = _kkt_residuals(nlp, res.x[k])
+        assert cv <= 1e-4 and bv <= 1e-12, (k, cv, bv)
+    # batch-composition invariance: problem 5 alone == problem 5 inside the batch
+    solo = ctx.solve(_native.PackedBatch([insts[5]]))
+    assert np.array_equal(solo.x[0], res.x[5])
+    # determinism
+    again = ctx.solve(pk)
+    assert np.array_equal(again.x, res.x)

@@ -1,0 +1,7 @@
+#!/bin/bash
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD FAIL; tail -20 gpurun_out/build.log; exit 1; }
+timeout -k 10 300 python tools/gpu_quick.py B 256 > gpurun_out/quickB.log 2>&1; echo "quickB rc=$?"; cat gpurun_out/quickB.log
+timeout -k 10 400 python tools/gpu_quick.py C 1024 > gpurun_out/quickC.log 2>&1; echo "quickC rc=$?"; cat gpurun_out/quickC.log
