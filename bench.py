@@ -1,0 +1,184 @@
+"""Headline benchmark: headland-turn OBCA solves/sec (batch, N=80, 6 obs).
+
+Workload (BASELINE.json configs[3], "D"): randomized row-spacing / heading
+headlands, horizon N=80, M=6 convex obstacles, K=1 vehicle body, time-scaling
+on; 4096 problems per GPU (weak scaling: 32768 at 8 GPUs).  A "step" is one
+batched solve of all of a rank's problems to IPOPT convergence
+(libhtp.so htp_obca_solve_batch_device, inputs resident in HBM).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config D]
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU; each rank
+solves its own contiguous slice of problem ids (no data-path collective); the
+timed region is bracketed by barrier + synchronize and the max over ranks is
+reported.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from headland_trajectory_planning_amd import _native, costmodel, synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def _gen(args):
+    pid, N, M, imp = args
+    return synth.make_instance(pid, N=N, M=M, implement=imp)
+
+
+def make_batch(pids, N, M, imp):
+    if len(pids) <= 64:
+        return [_gen((p, N, M, imp)) for p in pids]
+    import multiprocessing as mp
+    nproc = max(1, min(16, (os.cpu_count() or 4)))
+    with mp.get_context("fork").Pool(nproc) as pool:
+        return pool.map(_gen, [(p, N, M, imp) for p in pids], chunksize=32)
+
+
+def cpu_baseline(N, M, imp, budget_s=25.0):
+    """Oracle ("port"): numpy IPOPT restatement with the structured KKT solve,
+    one core, on the first problems of the same workload until the budget."""
+    from oracle.ipm import IpoptRestatement
+    from oracle.nlp import ObcaNLP
+    from oracle.structured import StructuredKKT
+    t0 = time.perf_counter()
+    done = 0
+    iters = 0
+    while time.perf_counter() - t0 < budget_s and done < 8:
+        inst = synth.make_instance(done, N=N, M=M, implement=imp)
+        nlp = ObcaNLP(inst)
+        sol = IpoptRestatement(nlp, kkt=StructuredKKT(nlp)).solve()
+        iters += sol["iters"]
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "solves/s", "cores": 1, "kind": "port",
+            "sample": f"{done} problem(s) (pids 0..{done - 1}) of the same workload solved to convergence by "
+                      f"oracle/ipm.py + oracle/structured.py (numpy, 1 core) in {dt:.1f} s; {iters} IPM iterations"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="D")
+    ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=25.0)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", init_method="env://")
+    dev = torch.device("cuda", local)
+
+    _, N, M, imp = synth.CONFIGS[args.config]
+    B = args.batch
+    pids = list(range(rank * B, (rank + 1) * B))
+    t = time.perf_counter()
+    insts = make_batch(pids, N, M, imp)
+    gen_s = time.perf_counter() - t
+    pk = _native.PackedBatch(insts)
+
+    def dt_(a):
+        return None if a is None else torch.from_numpy(a).to(dev)
+
+    dev_in = {k: dt_(getattr(pk, k)) for k in ("traj", "obs_A", "obs_b", "body_G", "body_g", "params",
+                                                "init_control", "init_mu", "init_lambda")}
+    ptrs = {k: (v.data_ptr() if v is not None else None) for k, v in dev_in.items()}
+    x_out = torch.empty((B, pk.n_var), dtype=torch.float64, device=dev)
+    obj = torch.empty(B, dtype=torch.float64, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+    iters = torch.empty(B, dtype=torch.int32, device=dev)
+    nfac = torch.empty(B, dtype=torch.int32, device=dev)
+    err = torch.empty(B, dtype=torch.float64, device=dev)
+    outp = {"x": x_out.data_ptr(), "objective": obj.data_ptr(), "status": status.data_ptr(),
+            "iterations": iters.data_ptr(), "n_factor": nfac.data_ptr(), "nlp_error": err.data_ptr()}
+    ctx = _native.Context(local)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ctx.solve_device(pk, ptrs, outp, stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        torch.cuda.synchronize(dev)          # events of this launch are complete
+        kernel_ms.append(ctx.last_kernel_ms())
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    it_np = iters.cpu().numpy()
+    st_np = status.cpu().numpy()
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        tot = torch.tensor([float(it_np.sum()), float(np.isin(st_np, [0, 1]).sum())], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot)
+        all_iters, all_ok = tot.tolist()
+    else:
+        all_iters, all_ok = float(it_np.sum()), float(np.isin(st_np, [0, 1]).sum())
+    total_solves = B * world * args.steps
+    value = total_solves / elapsed
+
+    topt = pk.time_opt
+    biter = int(costmodel.bytes_per_iteration(N, M, int(pk.K), int(topt), [int(e) for e in pk.obs_edges],
+                                              [int(e) for e in pk.body_edges]))
+    launch_bytes = biter * float(it_np.sum())     # this rank's launch
+    avg_ms = float(np.mean(kernel_ms))
+    achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    tf = os.environ.get("HTP_TRAFFIC_JSON")
+    if tf and os.path.exists(tf):
+        traffic = json.load(open(tf)).get("bytes_per_launch")
+
+    line = {
+        "metric": "headland-turn solves/sec (batch, N=80, 6 obs) at 1/2/4/8 MI355X",
+        "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (Philox-seeded orchard headlands, synth.py)",
+        "config": {"workload": f"config {args.config}: {B} problems/GPU, N={N} horizon, M={M} obstacles, "
+                               f"K={pk.K} bodies ({imp}), time-opt on; IPOPT-restated IPM to tol 1e-8",
+                   "batch_per_gpu": B, "global_batch": B * world, "N": N, "M": M, "K": pk.K,
+                   "parallelism": f"problem-sharded x{world}"},
+        "solver": {"success_rate": all_ok / (B * world), "mean_iters": all_iters / (B * world),
+                   "p99_iters_rank0": float(np.percentile(it_np, 99)), "max_iters_rank0": int(it_np.max()),
+                   "gen_s": gen_s},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "bytes_per_iter_per_problem": biter, "kernel_ms_avg": avg_ms},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(N, M, imp, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(line, default=float), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

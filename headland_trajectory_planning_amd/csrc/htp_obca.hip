@@ -138,7 +138,13 @@ int htp_set_option(htp_ctx* ctx, const char* name, double v) {
   return 0;
 }
 
-double htp_last_kernel_ms(htp_ctx* c) { return c ? c->last_ms : 0.0; }
+double htp_last_kernel_ms(htp_ctx* c) {
+  if (!c || !c->ev1) return 0.0;
+  if (hipEventSynchronize(c->ev1) != hipSuccess) return c->last_ms;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_ms = ms;
+  return c->last_ms;
+}
 
 // Diagnostic: per-problem phase cycle counters of the last solve ([batch][6] int64;
 // local sweeps, stage assembly, stage chain, KKT solves, total, reserved).

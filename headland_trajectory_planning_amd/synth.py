@@ -93,29 +93,26 @@ def dubins_shortest(q0, q1, r):
 
 
 def dubins_sample(q0, r, name, seg, s):
-    """Pose + curvature at arc lengths s (metres) along a Dubins word."""
-    s = np.asarray(s, dtype=np.float64)
-    out = np.zeros((s.size, 4))
-    for j, sj in enumerate(s):
-        t = sj / r
-        x, y, th = 0.0, 0.0, q0[2]
-        kap = 0.0
-        for typ, ln in zip(name, seg):
-            st = min(t, ln)
-            if typ == "L":
-                x, y, th = x + math.sin(th + st) - math.sin(th), y - math.cos(th + st) + math.cos(th), th + st
-                kap = 1.0 / r
-            elif typ == "R":
-                x, y, th = x - math.sin(th - st) + math.sin(th), y + math.cos(th - st) - math.cos(th), th - st
-                kap = -1.0 / r
-            else:
-                x, y = x + math.cos(th) * st, y + math.sin(th) * st
-                kap = 0.0
-            t -= st
-            if t <= 0:
-                break
-        out[j] = (q0[0] + x * r, q0[1] + y * r, th, kap)
-    return out
+    """Pose + curvature at arc lengths s (metres) along a Dubins word (vectorised)."""
+    t = np.asarray(s, dtype=np.float64) / r
+    x = np.zeros_like(t)
+    y = np.zeros_like(t)
+    th = np.full_like(t, q0[2])
+    kap = np.zeros_like(t)
+    rem = t.copy()
+    for typ, ln in zip(name, seg):
+        st = np.minimum(rem, ln)
+        act = rem > 0
+        if typ == "L":
+            nx, ny, nth, k = x + np.sin(th + st) - np.sin(th), y - np.cos(th + st) + np.cos(th), th + st, 1.0 / r
+        elif typ == "R":
+            nx, ny, nth, k = x - np.sin(th - st) + np.sin(th), y + np.cos(th - st) - np.cos(th), th - st, -1.0 / r
+        else:
+            nx, ny, nth, k = x + np.cos(th) * st, y + np.sin(th) * st, th, 0.0
+        x, y, th = np.where(act, nx, x), np.where(act, ny, y), np.where(act, nth, th)
+        kap = np.where(act, k, kap)
+        rem = rem - st
+    return np.stack([q0[0] + x * r, q0[1] + y * r, th, kap], axis=1)
 
 
 # ------------------------------------------------------------ angle helpers
@@ -136,23 +133,28 @@ def process_angle(raw):
 
 
 # ------------------------------------------------------------- polygon ops
-def _poly_at(poly, pose):
-    c, s = math.cos(pose[2]), math.sin(pose[2])
-    Rm = np.array([[c, -s], [s, c]])
-    return poly @ Rm.T + np.array(pose[:2])
+def _polys_at(poly, poses):
+    """poly (k,2) placed at every pose (P,3) -> (P,k,2)."""
+    c, s = np.cos(poses[:, 2]), np.sin(poses[:, 2])
+    px = poly[None, :, 0] * c[:, None] - poly[None, :, 1] * s[:, None] + poses[:, 0:1]
+    py = poly[None, :, 0] * s[:, None] + poly[None, :, 1] * c[:, None] + poses[:, 1:2]
+    return np.stack([px, py], axis=2)
 
 
-def _sat_gap(P, Q):
-    """Separating-axis gap between convex polygons (>0: disjoint)."""
-    best = -np.inf
-    for poly in (P, Q):
-        E = np.roll(poly, -1, axis=0) - poly
-        nrm = np.stack([E[:, 1], -E[:, 0]], axis=1)
-        nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
-        pa, pb = P @ nrm.T, Q @ nrm.T
-        gap = np.maximum(pb.min(0) - pa.max(0), pa.min(0) - pb.max(0))
-        best = max(best, gap.max())
-    return best
+def _min_sat_gap(F, Q):
+    """Smallest separating-axis gap between each convex polygon F[p] (P,k,2)
+    and the convex polygon Q (m,2); >0 means every pair is disjoint."""
+    def axes(poly):  # (..., e, 2) unit outward-ish normals
+        E = np.roll(poly, -1, axis=-2) - poly
+        nrm = np.stack([E[..., 1], -E[..., 0]], axis=-1)
+        return nrm / np.linalg.norm(nrm, axis=-1, keepdims=True)
+    best = np.full(F.shape[0], -np.inf)
+    for ax in (axes(F), np.broadcast_to(axes(Q), (F.shape[0],) + Q.shape)):
+        pa = np.einsum("pkd,ped->pke", F, ax)            # (P,k,e)
+        pb = np.einsum("md,ped->pme", Q, ax)             # (P,m,e)
+        gap = np.maximum(pb.min(1) - pa.max(1), pa.min(1) - pb.max(1))  # (P,e)
+        best = np.maximum(best, gap.max(1))
+    return best.min()
 
 
 def _rect(x0, x1, y0, y1):
@@ -194,8 +196,8 @@ def make_instance(pid, N=80, M=6, implement="none", key=20251015, **over):
         Lp = sum(seg) * r_min
         smp = dubins_sample(q0, r_min, name, seg, np.linspace(0.0, Lp, N))
         # footprint of the warm start (every pose, body + implements)
-        foot = [_poly_at(p, pose) for pose in smp[:, :3] for p in polys]
-        allpts = np.vstack(foot)
+        foot = [_polys_at(p, smp[:, :3]) for p in polys]
+        allpts = np.concatenate([f.reshape(-1, 2) for f in foot])
         x_b = allpts[:, 0].min() - margin
         obstacles = [_rect(x_b - 2.0, x_b, ys0.min() - 8.0, ys0.max() + 8.0)]
         row_order = list(range(s_row + 1, e_row + 1)) + [s_row, e_row + 1]
@@ -206,7 +208,7 @@ def make_instance(pid, N=80, M=6, implement="none", key=20251015, **over):
                      for r in row_order]
         up = _rect(xs0.min() - 8.0, xs0.max() + row_len + 8.0, ys0.max() + row_w, ys0.max() + row_w + 1.0)
         cand = obstacles + row_rects + [up]
-        ok = all(_sat_gap(f, o) > 0.02 for o in cand[:M] for f in foot)
+        ok = all(_min_sat_gap(f, o) > 0.02 for o in cand[:M] for f in foot)
         if ok:
             break
     cand = cand[:M]
