@@ -25,7 +25,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from headland_trajectory_planning_amd import _native, costmodel, synth  # noqa: E402
+from headland_trajectory_planning_amd import _native, costmodel, sharding, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -35,11 +35,11 @@ def _gen(args):
     return synth.make_instance(pid, N=N, M=M, implement=imp)
 
 
-def make_batch(pids, N, M, imp):
-    if len(pids) <= 64:
+def make_batch(pids, N, M, imp, procs=16):
+    if len(pids) <= 64 or procs <= 1:
         return [_gen((p, N, M, imp)) for p in pids]
     import multiprocessing as mp
-    nproc = max(1, min(16, (os.cpu_count() or 4)))
+    nproc = max(1, min(procs, (os.cpu_count() or 4)))
     with mp.get_context("fork").Pool(nproc) as pool:
         return pool.map(_gen, [(p, N, M, imp) for p in pids], chunksize=32)
 
@@ -74,6 +74,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
+    ap.add_argument("--gen-procs", type=int, default=16, help="CPU worker processes for instance generation")
     args = ap.parse_args()
 
     import torch
@@ -89,9 +90,9 @@ def main():
 
     _, N, M, imp = synth.CONFIGS[args.config]
     B = args.batch
-    pids = list(range(rank * B, (rank + 1) * B))
+    pids = sharding.rank_pids(rank, B)
     t = time.perf_counter()
-    insts = make_batch(pids, N, M, imp)
+    insts = make_batch(pids, N, M, imp, args.gen_procs)
     gen_s = time.perf_counter() - t
     pk = _native.PackedBatch(insts)
 
@@ -133,15 +134,8 @@ def main():
     elapsed = time.perf_counter() - t0
     it_np = iters.cpu().numpy()
     st_np = status.cpu().numpy()
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        tot = torch.tensor([float(it_np.sum()), float(np.isin(st_np, [0, 1]).sum())], dtype=torch.float64, device=dev)
-        dist.all_reduce(tot)
-        all_iters, all_ok = tot.tolist()
-    else:
-        all_iters, all_ok = float(it_np.sum()), float(np.isin(st_np, [0, 1]).sum())
+    elapsed, all_iters, all_ok = sharding.reduce_stats(dist, dev, elapsed, float(it_np.sum()),
+                                                       float(np.isin(st_np, [0, 1]).sum()))
     total_solves = B * world * args.steps
     value = total_solves / elapsed
 
@@ -152,9 +146,14 @@ def main():
     avg_ms = float(np.mean(kernel_ms))
     achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
     traffic = None
-    tf = os.environ.get("HTP_TRAFFIC_JSON")
+    # HBM bytes per launch measured with rocprofv3 PMC passes (tools/profile.sh ->
+    # profiles/*_traffic.json) for this exact workload; scaled to this launch's
+    # iteration count (bytes per problem-iteration x iterations).
+    tf = os.environ.get("HTP_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r01_traffic.json"))
     if tf and os.path.exists(tf):
-        traffic = json.load(open(tf)).get("bytes_per_launch")
+        tj = json.load(open(tf))
+        if tj.get("workload") == args.config and tj.get("batch") == B and tj.get("bytes_per_problem_iter"):
+            traffic = tj["bytes_per_problem_iter"] * float(it_np.sum())
 
     line = {
         "metric": "headland-turn solves/sec (batch, N=80, 6 obs) at 1/2/4/8 MI355X",

@@ -1,0 +1,24 @@
+"""Problem sharding across GPUs (one process per GPU).
+
+Problems are independent, so rank r of W solves the contiguous id slice
+[r*B, (r+1)*B) (weak scaling: B problems per GPU).  Problem ids seed the
+generator (Philox key [20251015, pid]), so a problem is identical at any world
+size.  The only collectives are the timing barrier and these two tiny
+reductions (RCCL on GPUs, gloo on CPU); nothing is exchanged on the data path.
+"""
+
+
+def rank_pids(rank, per_rank):
+    return list(range(rank * per_rank, (rank + 1) * per_rank))
+
+
+def reduce_stats(dist, device, elapsed, iters_sum, ok_sum):
+    """-> (max elapsed over ranks, total iterations, total converged)."""
+    if dist is None:
+        return float(elapsed), float(iters_sum), float(ok_sum)
+    import torch
+    t = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    s = torch.tensor([float(iters_sum), float(ok_sum)], dtype=torch.float64, device=device)
+    dist.all_reduce(s)
+    return float(t.item()), float(s[0].item()), float(s[1].item())
