@@ -222,9 +222,9 @@ class Context:
         return self.lib.htp_last_kernel_ms(self.ctx)
 
     def last_cycles(self, batch):
-        """[batch, 6] shader-cycle counters: local sweeps, stage assembly,
-        stage chain, KKT solves, total, reserved."""
-        out = np.zeros((batch, 6), dtype=np.int64)
+        """[batch, 8] shader-cycle counters: local sweeps, stage assembly,
+        stage chain, KKT solves, total, errors+grad_lag, line search, update+re-eval."""
+        out = np.zeros((batch, 8), dtype=np.int64)
         if self.lib.htp_last_cycles(self.ctx, out.ctypes.data, int(batch)) != 0:
             raise RuntimeError(self.error())
         return out

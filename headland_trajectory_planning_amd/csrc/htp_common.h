@@ -87,7 +87,8 @@ struct Shape {
 struct Result {            // per problem
   int32_t status, iters, n_factor, pad;
   double objective, final_mu, nlp_error, sf;
-  int64_t cyc[6];          // shader cycles: local sweeps, stage assembly, stage chain, kkt solve, total, evals
+  int64_t cyc[8];          // shader cycles: local sweeps, assembly, stage chain, kkt solves, total,
+                           // errors+grad_lag, line search, update+re-eval
 };
 
 enum Status { ST_SUCCESS = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_RESTORATION = 3, ST_STEPFAIL = 4,

@@ -21,8 +21,12 @@ namespace {
 
 constexpr int LDS_D = 4 * NBMAX * NBMAX + 8 + 2 * 64;
 
+#ifndef HTP_WAVES_PER_EU
+#define HTP_WAVES_PER_EU 1
+#endif
+
 template <int EN, int EM>
-__global__ __launch_bounds__(64) void obca_solve_kernel(const Shape* __restrict__ shp, BatchView b,
+__global__ __launch_bounds__(64, HTP_WAVES_PER_EU) void obca_solve_kernel(const Shape* __restrict__ shp, BatchView b,
                                                         double* __restrict__ ws_all, int64_t ws_stride,
                                                         Result* __restrict__ res, double* __restrict__ xout,
                                                         int batch) {
@@ -153,7 +157,7 @@ int htp_last_cycles(htp_ctx* ctx, int64_t* out, int32_t batch) {
   std::vector<Result> r((size_t)batch);
   HIPCHK(hipMemcpy(r.data(), ctx->scratch, sizeof(Result) * (size_t)batch, hipMemcpyDeviceToHost));
   for (int p = 0; p < batch; ++p)
-    for (int k = 0; k < 6; ++k) out[(size_t)p * 6 + k] = r[(size_t)p].cyc[k];
+    for (int k = 0; k < 8; ++k) out[(size_t)p * 8 + k] = r[(size_t)p].cyc[k];
   return 0;
 }
 

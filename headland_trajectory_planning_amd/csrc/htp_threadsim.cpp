@@ -60,6 +60,8 @@ struct ThreadWave {
     return s;
   }
   long long clock() const { return 0; }
+  double uniform(double v) const { return v; }
+  int uniform_i(int v) const { return v; }
   double bcast(double v, int src) const {
     sync(); sh->red[lane] = v; sync();
     double r = sh->red[src];

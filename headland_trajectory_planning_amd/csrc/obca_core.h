@@ -19,6 +19,7 @@
 #include "htp_common.h"
 #include "dyn_gen.h"
 
+#define HTP_UNROLL _Pragma("unroll 4")
 #ifndef HTP_FI
 #define HTP_FI __attribute__((always_inline))
 #endif
@@ -117,7 +118,7 @@ struct ObcaSolver {
   double theta_min, theta_max;
   int n_factor;
   bool use_ric = false;
-  long long cyc[6];
+  long long cyc[8];
   // filter (wave-uniform): entries live in per-wave LDS (c.lds + FILT_OFF)
   static constexpr int FMAX = 64;
   static constexpr int FILT_OFF = 4 * NBMAX * NBMAX + 8;
@@ -198,6 +199,7 @@ struct ObcaSolver {
     const double dT = par(P_DT);
     const double Qs00 = 2 * par(P_Q00), Qs01 = par(P_Q01) + par(P_Q10), Qs11 = 2 * par(P_Q11);
     const double Rs00 = 2 * par(P_R00), Rs01 = par(P_R01) + par(P_R10), Rs11 = 2 * par(P_R11);
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) g[q] = 0.0;
     c.sync();
     for (int i = c.lane; i < N - 1; i += c.width) {
@@ -311,6 +313,7 @@ struct ObcaSolver {
     const gd* scE = A(L.scE);
     const gd* scI = A(L.scI);
     gd* pr = A(L.pairR);
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) out[q] = 0.0;
     c.sync();
     for (int p = c.lane; p < D.P; p += c.width) {
@@ -383,6 +386,7 @@ struct ObcaSolver {
     const double vmax = dabs(par(P_MAXV)), smax = dabs(par(P_MAXSTEER));
     const double amax = dabs(par(P_MAXACC)), wmax = dabs(par(P_MAXSR));
     const double twopi = 2.0 * M_PI;
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) {
       double lo = -HTP_INF, hi = HTP_INF, v0 = 0.0;
       if (q < D.oU) {
@@ -423,6 +427,7 @@ struct ObcaSolver {
     gd* g = A(L.gf);
     eval_grad_f(x, g, 1.0);
     double mg = 0.0;
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) mg = dmax(mg, dabs(g[q]));
     mg = c.maxv(mg);
     sf = mg > o.scaling_max_gradient ? dmax(o.scaling_min_value, o.scaling_max_gradient / mg) : 1.0;
@@ -486,6 +491,7 @@ struct ObcaSolver {
     gd* xL = A(L.xL);
     gd* xU = A(L.xU);
     const double rf = o.bound_relax_factor;
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) {
       double lo = xL[q], hi = xU[q];
       const bool hl = finite_(lo), hu = finite_(hi);
@@ -519,6 +525,7 @@ struct ObcaSolver {
     gd* dU = A(L.dU);
     const gd* d = A(L.d);
     const gd* scI = A(L.scI);
+    HTP_UNROLL
     for (int r = c.lane; r < D.md; r += c.width) {
       double lo, hi;
       if ((r & 1) == 0) { lo = 0.0; hi = 1.0; } else { lo = dmn; hi = HTP_INF; }
@@ -952,8 +959,8 @@ struct ObcaSolver {
         sh[1] = kstep;
       }
       c.sync();
-      kp = (int)sh[0];
-      kstep = (int)sh[1];
+      kp = c.uniform_i((int)sh[0]);
+      kstep = c.uniform_i((int)sh[1]);
       c.sync();
       const int kk = k + kstep - 1;
       if (kp != kk) {  // LAPACK-style interchange of rows/cols kk, kp inside the trailing block A(k:n,k:n)
@@ -1173,23 +1180,44 @@ struct ObcaSolver {
       c.sync();
       for (int e = c.lane; e < 64; e += c.width) Ps[e] = Pc[e];
     }
-    for (int i = N - 2; i >= 0; --i) {
-      // load stage data
-      const gd* Kst = A(L.Kst) + (int64_t)i * nb * nb;
-      const gd* On = A(L.Off) + (int64_t)(i + 1) * nb * nb;
-      const gd* Op = A(L.Off) + (int64_t)i * nb * nb;
-      for (int e = c.lane; e < 64; e += c.width) {
+    // stage records (H_w 64 | J 40 | C_{i-1} 6), prefetched one stage ahead
+    ld* fb0 = c.lds + 400;
+    ld* fb1 = c.lds + 512;
+    auto rec = [&](int i, int e) -> double {
+      if (e < 64) {
         const int r = e / 8, q = e % 8;
-        Hw[e] = (r < D.nw && q < D.nw) ? Kst[(NS + r) * nb + NS + q] : 0.0;
+        return (r < D.nw && q < D.nw) ? A(L.Kst)[(int64_t)i * nb * nb + (NS + r) * nb + NS + q] : 0.0;
       }
-      for (int e = c.lane; e < 40; e += c.width) {
-        const int k = e / 8, j = e % 8;
-        Jm[e] = (j < D.nw) ? -On[k * nb + NS + j] / scE[D.eDyn + NS * i + k] : 0.0;
+      if (e < 104) {
+        const int k = (e - 64) / 8, j = (e - 64) % 8;
+        return (j < D.nw) ? -A(L.Off)[(int64_t)(i + 1) * nb * nb + k * nb + NS + j] / scE[D.eDyn + NS * i + k] : 0.0;
       }
-      for (int e = c.lane; e < 6; e += c.width) {
-        const int a = e / 3, b = e % 3;
-        Cb[e] = (i >= 1 && b < nv) ? Op[(NS + 5 + a) * nb + NS + 5 + b] : 0.0;
+      if (e < 110) {
+        const int a = (e - 104) / 3, b = (e - 104) % 3;
+        return (i >= 1 && b < nv) ? A(L.Off)[(int64_t)i * nb * nb + (NS + 5 + a) * nb + NS + 5 + b] : 0.0;
       }
+      return 0.0;
+    };
+    constexpr int PF = (112 + Ctx::width - 1) / Ctx::width;
+    if (N >= 2)
+      for (int e = c.lane; e < 112; e += c.width) fb0[e] = rec(N - 2, e);
+    c.sync();
+    for (int i = N - 2; i >= 0; --i) {
+      ld* cur = ((N - 2 - i) & 1) ? fb1 : fb0;
+      ld* nxt = ((N - 2 - i) & 1) ? fb0 : fb1;
+      double pre[PF];
+      for (int u = 0; u < PF; ++u) {
+        const int e = c.lane + u * c.width;
+        pre[u] = (i > 0 && e < 112) ? rec(i - 1, e) : 0.0;
+      }
+      for (int e = c.lane; e < 64; e += c.width) Hw[e] = cur[e];
+      for (int e = c.lane; e < 40; e += c.width) Jm[e] = cur[64 + e];
+      for (int e = c.lane; e < 6; e += c.width) Cb[e] = cur[104 + e];
+      if (i > 0)
+        for (int u = 0; u < PF; ++u) {
+          const int e = c.lane + u * c.width;
+          if (e < 112) nxt[e] = pre[u];
+        }
       c.sync();
       // PJx = P[:,0:5] Jx ; PB = P[:,0:5] Jv + P[:,5:5+nv]
       for (int e = c.lane; e < nz * (NS + nv); e += c.width) {
@@ -1258,108 +1286,163 @@ struct ObcaSolver {
     return bad;
   }
 
-  // V (block order [y|x|u|tau]) -> X (same order) with the Riccati factor
-  HTP_HD HTP_FI void riccati_solve(const gd* V, gd* X) {
+  // V (block order [y|x|u|tau]) -> X (same order) with the Riccati factor.
+  // Each stage's inputs are packed into a fixed 128/192-entry record that the
+  // wave loads with one coalesced round trip, one stage ahead of use
+  // (double-buffered in LDS), so the sequential passes are LDS-latency bound.
+  static constexpr int RB = 128;  // backward record
+  static constexpr int RF = 192;  // forward record
+
+  HTP_HD HTP_FI double rec_back(int i, int e, const gd* V) const {
+    const int nb = D.nb, nv = D.nw - NS, nz = NS + nv;
+    const gd* scE = A(L.scE);
+    if (e < 40) {  // P_{i+1}[r][t], r < 8, t < 5
+      const int r = e / 5, t = e % 5;
+      return (r < nz) ? A(L.LD)[(int64_t)(i + 1) * nb * nb + r * 8 + t] : 0.0;
+    }
+    if (e < 80) {  // J_i[k][j] (unscaled)
+      const int k = (e - 40) / 8, j = (e - 40) % 8;
+      return (j < D.nw) ? -A(L.Off)[(int64_t)(i + 1) * nb * nb + k * nb + NS + j] / scE[D.eDyn + NS * i + k] : 0.0;
+    }
+    if (e < 85) { const int k = e - 80; return V[(int64_t)(i + 1) * nb + k] / scE[D.eDyn + NS * i + k]; }
+    if (e < 90) return V[(int64_t)i * nb + NS + (e - 85)];
+    if (e < 93) return (e - 90 < nv) ? V[(int64_t)i * nb + NS + NS + (e - 90)] : 0.0;
+    if (e >= 96 && e < 120) return A(L.LD)[(int64_t)i * nb * nb + 64 + (e - 96)];
+    return 0.0;
+  }
+
+  HTP_HD HTP_FI double rec_fwd(int i, int e, const gd* V, const gd* X) const {
     const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
     const gd* scE = A(L.scE);
-    ld* pv = c.lds;          // p_{i+1} (8)
-    ld* wv = c.lds + 8;      // w (8)
-    ld* rt = c.lds + 16;     // rt (3)
-    ld* zv = c.lds + 24;     // z (8)
-    ld* vv = c.lds + 32;     // v (3)
-    // backward: p_{N-1} = [q_{N-1}; 0]
-    {
-      gd* Xl = X + (int64_t)(N - 1) * nb;
-      const gd* Vl = V + (int64_t)(N - 1) * nb;
-      for (int k = c.lane; k < 8; k += c.width) {
-        const double val = (k < NS) ? Vl[NS + k] : 0.0;
-        pv[k] = val;
-        Xl[k] = val;
-      }
-      c.sync();
+    const int64_t slot = (int64_t)i * nb * nb;
+    if (e < 40) return A(L.LD)[slot + (e / 8) * 8 + (e % 8)];          // P_i rows 0..4
+    if (e < 48) return (e - 40 < nz) ? X[(int64_t)i * nb + (e - 40)] : 0.0;  // p_i
+    if (e < 51) return (i < N - 1 && e - 48 < nv) ? X[(int64_t)i * nb + nz + (e - 48)] : 0.0;  // rt_i
+    if (e < 60) return (i < N - 1) ? A(L.LD)[slot + 88 + (e - 51)] : 0.0;  // chol(Rt_i)
+    if (e < 84) return (i < N - 1) ? A(L.LD)[slot + 64 + (e - 60)] : 0.0;  // K_i
+    if (e < 124) {                                                       // J_i
+      if (i >= N - 1) return 0.0;
+      const int k = (e - 84) / 8, j = (e - 84) % 8;
+      return (j < D.nw) ? -A(L.Off)[(int64_t)(i + 1) * nb * nb + k * nb + NS + j] / scE[D.eDyn + NS * i + k] : 0.0;
     }
+    if (e < 129) {                                                       // e_{i+1}
+      if (i >= N - 1) return 0.0;
+      const int k = e - 124;
+      return V[(int64_t)(i + 1) * nb + k] / scE[D.eDyn + NS * i + k];
+    }
+    if (e < 134) {                                                       // 1/sc of y_i rows
+      const int ybase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
+      return 1.0 / scE[ybase + (e - 129)];
+    }
+    return 0.0;
+  }
+
+  HTP_HD HTP_FI void riccati_solve(const gd* V, gd* X) {
+    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
+    ld* buf0 = c.lds;             // two records (RF each)
+    ld* buf1 = c.lds + RF;
+    ld* pv = c.lds + 2 * RF;      // p (8)
+    ld* wv = pv + 8;              // w (8)
+    ld* rt = pv + 16;             // rt (3)
+    ld* zv = pv + 24;             // z (8)
+    ld* vv = pv + 32;             // v (3)
+    ld* yv = pv + 40;             // y (5)
+    constexpr int PB = (RF + Ctx::width - 1) / Ctx::width;
+    // ---------------- backward: p_{N-1} = [q_{N-1}; 0]
+    for (int k = c.lane; k < 8; k += c.width) {
+      const double val = (k < NS) ? V[(int64_t)(N - 1) * nb + NS + k] : 0.0;
+      pv[k] = val;
+      X[(int64_t)(N - 1) * nb + k] = val;
+    }
+    if (N >= 2)
+      for (int e = c.lane; e < RB; e += c.width) buf0[e] = rec_back(N - 2, e, V);
+    c.sync();
     for (int i = N - 2; i >= 0; --i) {
-      const gd* Pn = A(L.LD) + (int64_t)(i + 1) * nb * nb;  // P_{i+1}
-      const gd* Pi = A(L.LD) + (int64_t)i * nb * nb;        // K_i at +64
-      const gd* On = A(L.Off) + (int64_t)(i + 1) * nb * nb;
-      const gd* Vn = V + (int64_t)(i + 1) * nb;
-      const gd* Vi = V + (int64_t)i * nb;
-      // w = p_{i+1} - P_{i+1}[:, 0:5] e_{i+1}
-      for (int r = c.lane; r < nz; r += c.width) {
+      ld* cur = ((N - 2 - i) & 1) ? buf1 : buf0;
+      ld* nxt = ((N - 2 - i) & 1) ? buf0 : buf1;
+      double pre[PB];
+      for (int u = 0; u < PB; ++u) {
+        const int e = c.lane + u * c.width;
+        pre[u] = (i > 0 && e < RB) ? rec_back(i - 1, e, V) : 0.0;
+      }
+      for (int r = c.lane; r < nz; r += c.width) {  // w = p - P e
         double acc = pv[r];
-        for (int t = 0; t < NS; ++t) acc -= Pn[r * 8 + t] * (Vn[t] / scE[D.eDyn + NS * i + t]);
+        for (int t = 0; t < NS; ++t) acc -= cur[r * 5 + t] * cur[80 + t];
         wv[r] = acc;
       }
       c.sync();
-      // rt = r_i + Jv' w[0:5] + w[5:5+nv]
-      for (int a = c.lane; a < nv; a += c.width) {
-        double acc = Vi[NS + NS + a] + wv[NS + a];
-        for (int t = 0; t < NS; ++t) acc += (-On[t * nb + NS + NS + a] / scE[D.eDyn + NS * i + t]) * wv[t];
-        rt[a] = acc;
+      for (int a2 = c.lane; a2 < nv; a2 += c.width) {  // rt = r + Jv' w + w_v
+        double acc = cur[90 + a2] + wv[NS + a2];
+        for (int t = 0; t < NS; ++t) acc += cur[40 + t * 8 + NS + a2] * wv[t];
+        rt[a2] = acc;
       }
       c.sync();
-      // p_i = q_i + Jx' w[0:5] + K' rt ;  k_i = Rt^-1 rt = -(K... ) -> stored as solve of Rt
       gd* Xi = X + (int64_t)i * nb;
-      for (int r = c.lane; r < nz; r += c.width) {
-        double acc = (r < NS) ? Vi[NS + r] : 0.0;
+      double pnew[8];
+      for (int r = c.lane; r < nz; r += c.width) {  // p = q + Jx' w + K' rt
+        double acc = (r < NS) ? cur[85 + r] : 0.0;
         if (r < NS)
-          for (int t = 0; t < NS; ++t) acc += (-On[t * nb + NS + r] / scE[D.eDyn + NS * i + t]) * wv[t];
-        for (int a = 0; a < nv; ++a) acc += Pi[64 + a * 8 + r] * rt[a];
-        Xi[r] = acc;  // p_i
+          for (int t = 0; t < NS; ++t) acc += cur[40 + t * 8 + r] * wv[t];
+        for (int a2 = 0; a2 < nv; ++a2) acc += cur[96 + a2 * 8 + r] * rt[a2];
+        pnew[(r - c.lane) / c.width] = acc;
+        Xi[r] = acc;
       }
-      for (int a = c.lane; a < nv; a += c.width) Xi[nz + a] = rt[a];  // rt_i (k_i = Rt^-1 rt later)
+      for (int a2 = c.lane; a2 < nv; a2 += c.width) Xi[nz + a2] = rt[a2];
       c.sync();
-      for (int r = c.lane; r < nz; r += c.width) pv[r] = Xi[r];
+      for (int r = c.lane; r < nz; r += c.width) pv[r] = pnew[(r - c.lane) / c.width];
+      if (i > 0)
+        for (int u = 0; u < PB; ++u) {
+          const int e = c.lane + u * c.width;
+          if (e < RB) nxt[e] = pre[u];
+        }
       c.sync();
     }
-    // forward: z_0 = [x_0; 0], v_i = Rt^-1 rt_i + K_i z_i, y_i = (p_i - P_i z_i)[0:5]
-    ld* pz = c.lds + 40;     // p_i (8)
-    ld* rr = c.lds + 48;     // rt_i (3)
-    ld* yv = c.lds + 56;     // y_i (5)
-    for (int k = c.lane; k < 8; k += c.width) zv[k] = (k < NS) ? V[k] / scE[k] : 0.0;
+    // ---------------- forward: z_0 = [x_0; 0]; v = Rt^-1 rt + K z; y = (p - P z)[0:5]
+    {
+      const gd* scE = A(L.scE);
+      for (int k = c.lane; k < 8; k += c.width) zv[k] = (k < NS) ? V[k] / scE[k] : 0.0;
+    }
+    for (int e = c.lane; e < RF; e += c.width) buf0[e] = rec_fwd(0, e, V, X);
     c.sync();
     for (int i = 0; i < N; ++i) {
-      const gd* Ps = A(L.LD) + (int64_t)i * nb * nb;
-      gd* Xi = X + (int64_t)i * nb;
-      const int ybase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
-      for (int k = c.lane; k < nz; k += c.width) pz[k] = Xi[k];
-      if (i < N - 1)
-        for (int a2 = c.lane; a2 < nv; a2 += c.width) rr[a2] = Xi[nz + a2];
-      c.sync();
+      ld* cur = (i & 1) ? buf1 : buf0;
+      ld* nxt = (i & 1) ? buf0 : buf1;
+      double pre[PB];
+      for (int u = 0; u < PB; ++u) {
+        const int e = c.lane + u * c.width;
+        pre[u] = (i + 1 < N && e < RF) ? rec_fwd(i + 1, e, V, X) : 0.0;
+      }
       for (int k = c.lane; k < NS; k += c.width) {
-        double acc = pz[k];
-        for (int t = 0; t < nz; ++t) acc -= Ps[k * 8 + t] * zv[t];
-        yv[k] = acc / scE[ybase + k];
+        double acc = cur[40 + k];
+        for (int t = 0; t < nz; ++t) acc -= cur[k * 8 + t] * zv[t];
+        yv[k] = acc * cur[129 + k];
       }
       if (i < N - 1) {
-        double kv[3] = {rr[0], nv > 1 ? rr[1] : 0.0, nv > 2 ? rr[2] : 0.0};
+        double kv[3] = {cur[48], cur[49], cur[50]};
         double Lc[9];
-        for (int e = 0; e < 9; ++e) Lc[e] = Ps[88 + e];
+        for (int e = 0; e < 9; ++e) Lc[e] = cur[51 + e];
         chol3_solve(Lc, nv, kv);
         for (int a2 = c.lane; a2 < nv; a2 += c.width) {
           double acc = kv[a2];
-          for (int t = 0; t < nz; ++t) acc += Ps[64 + a2 * 8 + t] * zv[t];
+          for (int t = 0; t < nz; ++t) acc += cur[60 + a2 * 8 + t] * zv[t];
           vv[a2] = acc;
         }
       }
       c.sync();
+      gd* Xi = X + (int64_t)i * nb;
       double zn[8];
-      if (i < N - 1) {
-        const gd* On = A(L.Off) + (int64_t)(i + 1) * nb * nb;
-        const gd* Vn = V + (int64_t)(i + 1) * nb;
+      if (i < N - 1)
         for (int k = c.lane; k < nz; k += c.width) {
           double acc;
           if (k < NS) {
-            const double sk = scE[D.eDyn + NS * i + k];
-            acc = Vn[k] / sk;
-            for (int t = 0; t < NS; ++t) acc += (-On[k * nb + NS + t] / sk) * zv[t];
-            for (int a2 = 0; a2 < nv; ++a2) acc += (-On[k * nb + NS + NS + a2] / sk) * vv[a2];
+            acc = cur[124 + k];
+            for (int t = 0; t < NS; ++t) acc += cur[84 + k * 8 + t] * zv[t];
+            for (int a2 = 0; a2 < nv; ++a2) acc += cur[84 + k * 8 + NS + a2] * vv[a2];
           } else {
             acc = vv[k - NS];
           }
           zn[(k - c.lane) / c.width] = acc;
         }
-      }
       for (int k = c.lane; k < NS; k += c.width) {
         Xi[k] = yv[k];
         Xi[NS + k] = zv[k];
@@ -1369,8 +1452,12 @@ struct ObcaSolver {
       c.sync();
       if (i < N - 1) {
         for (int k = c.lane; k < nz; k += c.width) zv[k] = zn[(k - c.lane) / c.width];
-        c.sync();
+        for (int u = 0; u < PB; ++u) {
+          const int e = c.lane + u * c.width;
+          if (e < RF) nxt[e] = pre[u];
+        }
       }
+      c.sync();
     }
   }
 
@@ -1561,10 +1648,12 @@ struct ObcaSolver {
     const gd* xU = A(L.xU);
     const gd* dU = A(L.dU);
     int a = 0, b = 0, e = 0;
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) {
       a += finite_(xL[q]);
       b += finite_(xU[q]);
     }
+    HTP_UNROLL
     for (int r = c.lane; r < D.md; r += c.width) e += finite_(dU[r]);
     nbL = c.isum(a);
     nbU = c.isum(b);
@@ -1578,6 +1667,7 @@ struct ObcaSolver {
   HTP_HD HTP_FI void grad_lag_into(gd* out) {
     eval_jt(A(L.x), A(L.yc), A(L.yd), out);
     const gd* gf = A(L.gf);
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) out[q] += gf[q];
     c.sync();
   }
@@ -1590,11 +1680,13 @@ struct ObcaSolver {
     const gd* yc = A(L.yc); const gd* yd = A(L.yd);
     const gd* cc = A(L.c); const gd* dd = A(L.d);
     double dual = 0, comp = 0, zsum = 0, ysum = 0, pb = 0, pn = 0;
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) {
       dual = dmax(dual, dabs(gl[q] - zL[q] + zU[q]));
       if (finite_(xL[q])) { comp = dmax(comp, dabs((x[q] - xL[q]) * zL[q] - mu_)); zsum += dabs(zL[q]); }
       if (finite_(xU[q])) { comp = dmax(comp, dabs((xU[q] - x[q]) * zU[q] - mu_)); zsum += dabs(zU[q]); }
     }
+    HTP_UNROLL
     for (int r = c.lane; r < D.md; r += c.width) {
       dual = dmax(dual, dabs(-yd[r] - vL[r] + vU[r]));
       comp = dmax(comp, dabs((s[r] - dL[r]) * vL[r] - mu_));
@@ -1606,6 +1698,7 @@ struct ObcaSolver {
       if (finite_(dU[r])) v = dmax(v, dd[r] - dU[r]);
       pn = dmax(pn, v);
     }
+    HTP_UNROLL
     for (int r = c.lane; r < D.mc; r += c.width) {
       ysum += dabs(yc[r]);
       pb = dmax(pb, dabs(cc[r]));
@@ -1630,7 +1723,9 @@ struct ObcaSolver {
     const gd* scE = A(L.scE); const gd* scI = A(L.scI);
     const double dmn = par(P_DMIN);
     double v = 0;
+    HTP_UNROLL
     for (int r = c.lane; r < D.mc; r += c.width) v = dmax(v, dabs(cc[r]) / scE[r]);
+    HTP_UNROLL
     for (int r = c.lane; r < D.md; r += c.width) {
       const double g = dd[r] / scI[r];
       if ((r & 1) == 0) v = dmax(v, dmax(0.0 - g, g - 1.0));
@@ -1641,7 +1736,9 @@ struct ObcaSolver {
 
   HTP_HD HTP_FI double theta_of(const gd* cc, const gd* dd, const gd* s) const {
     double t = 0;
+    HTP_UNROLL
     for (int r = c.lane; r < D.mc; r += c.width) t += dabs(cc[r]);
+    HTP_UNROLL
     for (int r = c.lane; r < D.md; r += c.width) t += dabs(dd[r] - s[r]);
     return c.sum(t);
   }
@@ -1653,11 +1750,13 @@ struct ObcaSolver {
     const double kd = o.kappa_d * mu_;
     double lg = 0.0, lin = 0.0;
     int bad = 0;
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) {
       const bool hl = finite_(xL[q]), hu = finite_(xU[q]);
       if (hl) { const double v = x[q] - xL[q]; if (v <= 0) bad = 1; else lg += log(v); if (!hu) lin += v; }
       if (hu) { const double v = xU[q] - x[q]; if (v <= 0) bad = 1; else lg += log(v); if (!hl) lin += v; }
     }
+    HTP_UNROLL
     for (int r = c.lane; r < D.md; r += c.width) {
       const bool hu = finite_(dU[r]);
       const double v = s[r] - dL[r];
@@ -1678,6 +1777,7 @@ struct ObcaSolver {
     const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     const gd* gf = A(L.gf);
     const double kd = o.kappa_d * mu_;
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) {
       const bool hl = finite_(xL[q]), hu = finite_(xU[q]);
       double g = gf[q];
@@ -1687,6 +1787,7 @@ struct ObcaSolver {
       if (hu && !hl) g -= kd;
       gx[q] = g;
     }
+    HTP_UNROLL
     for (int r = c.lane; r < D.md; r += c.width) {
       const bool hu = finite_(dU[r]);
       double g = -mu_ / (s[r] - dL[r]);
@@ -1701,10 +1802,12 @@ struct ObcaSolver {
     const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
     const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     double a = 1.0;
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) {
       if (finite_(xL[q]) && dx[q] < 0) a = dmin(a, -tau * (x[q] - xL[q]) / dx[q]);
       if (finite_(xU[q]) && -dx[q] < 0) a = dmin(a, -tau * (xU[q] - x[q]) / (-dx[q]));
     }
+    HTP_UNROLL
     for (int r = c.lane; r < D.md; r += c.width) {
       if (ds[r] < 0) a = dmin(a, -tau * (s[r] - dL[r]) / ds[r]);
       if (finite_(dU[r]) && -ds[r] < 0) a = dmin(a, -tau * (dU[r] - s[r]) / (-ds[r]));
@@ -1720,6 +1823,7 @@ struct ObcaSolver {
     const gd* vL = A(L.vL); const gd* vU = A(L.vU);
     gd* dzL = A(L.dzL); gd* dzU = A(L.dzU); gd* dvL = A(L.dvL); gd* dvU = A(L.dvU);
     double a = 1.0;
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) {
       double t = 0.0, u = 0.0;
       if (finite_(xL[q])) { const double sl = x[q] - xL[q]; t = (mu - zL[q] * sl - zL[q] * dx[q]) / sl; if (t < 0) a = dmin(a, -tau * zL[q] / t); }
@@ -1727,6 +1831,7 @@ struct ObcaSolver {
       dzL[q] = t;
       dzU[q] = u;
     }
+    HTP_UNROLL
     for (int r = c.lane; r < D.md; r += c.width) {
       const double sl = s[r] - dL[r];
       const double t = (mu - vL[r] * sl - vL[r] * ds[r]) / sl;
@@ -1783,19 +1888,19 @@ struct ObcaSolver {
   }
 
   HTP_HD HTP_FI void run(Result& res) {
-    for (int k = 0; k < 6; ++k) cyc[k] = 0;
+    for (int k = 0; k < 8; ++k) cyc[k] = 0;
     const long long t0 = c.clock();
     initialize();
     iterate(res);
     if (c.lane == 0) {
-      for (int k = 0; k < 6; ++k) res.cyc[k] = cyc[k];
+      for (int k = 0; k < 8; ++k) res.cyc[k] = cyc[k];
       res.cyc[4] = c.clock() - t0;
     }
   }
 
   HTP_HD HTP_FI void initialize() {
     n_factor = 0;
-    for (int k = 0; k < 6; ++k) cyc[k] = 0;
+    for (int k = 0; k < 8; ++k) cyc[k] = 0;
     dw_last = 0.0;
     nfilt = 0;
     set_bounds_and_x0();
@@ -1814,16 +1919,20 @@ struct ObcaSolver {
     {
       const gd* xL = A(L.xL); const gd* xU = A(L.xU); const gd* dU = A(L.dU);
       gd* zL = A(L.zL); gd* zU = A(L.zU); gd* vL = A(L.vL); gd* vU = A(L.vU);
+      HTP_UNROLL
       for (int q = c.lane; q < D.n; q += c.width) {
         zL[q] = finite_(xL[q]) ? o.bound_mult_init_val : 0.0;
         zU[q] = finite_(xU[q]) ? o.bound_mult_init_val : 0.0;
       }
+      HTP_UNROLL
       for (int r = c.lane; r < D.md; r += c.width) {
         vL[r] = o.bound_mult_init_val;
         vU[r] = finite_(dU[r]) ? o.bound_mult_init_val : 0.0;
       }
       gd* yc = A(L.yc); gd* yd = A(L.yd);
+      HTP_UNROLL
       for (int r = c.lane; r < D.mc; r += c.width) yc[r] = 0.0;
+      HTP_UNROLL
       for (int r = c.lane; r < D.md; r += c.width) yd[r] = 0.0;
       c.sync();
     }
@@ -1841,20 +1950,27 @@ struct ObcaSolver {
         gd* bx = A(L.rx); gd* bs = A(L.rs); gd* bc = A(L.rc); gd* bd = A(L.rd);
         const gd* gf = A(L.gf);
         const gd* zL = A(L.zL); const gd* zU = A(L.zU); const gd* vL = A(L.vL); const gd* vU = A(L.vU);
+        HTP_UNROLL
         for (int q = c.lane; q < D.n; q += c.width) bx[q] = -(gf[q] - zL[q] + zU[q]);
+        HTP_UNROLL
         for (int r = c.lane; r < D.md; r += c.width) { bs[r] = -(-vL[r] + vU[r]); bd[r] = 0.0; }
+        HTP_UNROLL
         for (int r = c.lane; r < D.mc; r += c.width) bc[r] = 0.0;
         c.sync();
         kkt_solve(true, 0.0, 0.0, bx, bs, bc, bd, A(L.dx), A(L.ds), A(L.dyc), A(L.dyd));
         HTP_TRACE("[trace] LS solve\n");
         const gd* a1 = A(L.dyc); const gd* a2 = A(L.dyd);
         double mx = 0.0;
+        HTP_UNROLL
         for (int r = c.lane; r < D.mc; r += c.width) mx = dmax(mx, dabs(a1[r]));
+        HTP_UNROLL
         for (int r = c.lane; r < D.md; r += c.width) mx = dmax(mx, dabs(a2[r]));
         mx = c.maxv(mx);
         if (mx <= o.constr_mult_init_max) {
           gd* yc = A(L.yc); gd* yd = A(L.yd);
+          HTP_UNROLL
           for (int r = c.lane; r < D.mc; r += c.width) yc[r] = a1[r];
+          HTP_UNROLL
           for (int r = c.lane; r < D.md; r += c.width) yd[r] = a2[r];
         }
         c.sync();
@@ -1872,10 +1988,14 @@ struct ObcaSolver {
   HTP_HD HTP_FI void iterate(Result& res) {
     gd* x = A(L.x); gd* s = A(L.s);
     gd* cc = A(L.c); gd* dd = A(L.d);
+    // phi / theta of the current point are carried over from the accepted trial
+    // point (bitwise identical: x_new is computed by the same expression as x_trial)
+    double phi_cache = 0.0, mu_cache = -1.0, theta_cache = -1.0;
     int status = ST_MAXITER, it = 0, acc_count = 0;
     double nlp_err = 0.0;
     gd* gl = A(L.rx);
     for (it = 0; it <= o.max_iter; ++it) {
+      long long tq0 = c.clock();
       grad_lag_into(gl);
       Err e0 = errors(gl, 0.0);
       HTP_TRACE("[trace] it %d err dual=%g comp=%g prim=%g mu=%g\n", it, e0.dual, e0.comp, e0.prim_nlp, mu);
@@ -1903,6 +2023,7 @@ struct ObcaSolver {
         tau = dmax(o.tau_min, 1.0 - mu);
         nfilt = 0;
       }
+      cyc[5] += c.clock() - tq0;
       // Newton rhs: rx = grad_barrier + J'y ; rs = gbs - yd ; rc = c ; rd = d - s  (negated below)
       gd* gbx = A(L.sx);   // scratch for barrier gradient
       gd* gbs = A(L.ss);
@@ -1912,8 +2033,11 @@ struct ObcaSolver {
       {
         const gd* gf = A(L.gf);
         const gd* yd = A(L.yd);
+        HTP_UNROLL
         for (int q = c.lane; q < D.n; q += c.width) rx[q] = -(gl[q] - gf[q] + gbx[q]);
+        HTP_UNROLL
         for (int r = c.lane; r < D.md; r += c.width) { rs[r] = -(gbs[r] - yd[r]); rd[r] = -(dd[r] - s[r]); }
+        HTP_UNROLL
         for (int r = c.lane; r < D.mc; r += c.width) rc[r] = -cc[r];
         c.sync();
       }
@@ -1925,10 +2049,13 @@ struct ObcaSolver {
       kkt_solve(false, dw, dc, rx, rs, rc, rd, dx, ds, dyc, dyd);
       HTP_TRACE("[trace] solved\n");
       // line search
-      const double phi = barrier(x, s, mu);
-      const double theta = theta_of(cc, dd, s);
+      long long tls = c.clock();
+      const double phi = (mu_cache == mu) ? phi_cache : barrier(x, s, mu);
+      const double theta = (theta_cache >= 0.0) ? theta_cache : theta_of(cc, dd, s);
       double gBD = 0.0;
+      HTP_UNROLL
       for (int q = c.lane; q < D.n; q += c.width) gBD += gbx[q] * dx[q];
+      HTP_UNROLL
       for (int r = c.lane; r < D.md; r += c.width) gBD += gbs[r] * ds[r];
       gBD = c.sum(gBD);
       const double alpha_max = frac_primal(dx, ds);
@@ -1941,23 +2068,28 @@ struct ObcaSolver {
       auto is_ftype = [&](double a) { return gBD < 0 && a * pow(-gBD, o.s_phi) > o.delta * pow(theta, o.s_theta); };
       // keep the Newton rhs (x part) for SOC solves: copy into sx after gbx is consumed
       gd* rxk = A(L.sx);
+      HTP_UNROLL
       for (int q = c.lane; q < D.n; q += c.width) rxk[q] = rx[q];
       c.sync();
       gd* xt = A(L.xt); gd* st = A(L.st);
-      double alpha = alpha_max, a_primal = alpha, a_test = alpha, th_t = 0, ph_t = 0;
+      double alpha = alpha_max, a_primal = alpha, a_test = alpha, th_t = 0, ph_t = 0, th_acc = 0;
       bool accepted = false, soc_used = false, first = true;
       while (alpha >= a_min) {
+        HTP_UNROLL
         for (int q = c.lane; q < D.n; q += c.width) xt[q] = x[q] + alpha * dx[q];
+        HTP_UNROLL
         for (int r = c.lane; r < D.md; r += c.width) st[r] = s[r] + alpha * ds[r];
         c.sync();
         if (acceptable(alpha, xt, st, phi, theta, gBD, is_ftype(alpha), th_t, ph_t)) {
-          accepted = true; a_primal = alpha; a_test = alpha;
+          accepted = true; a_primal = alpha; a_test = alpha; th_acc = th_t;
           break;
         }
         if (first && th_t >= theta && o.max_soc > 0) {
           gd* csoc = A(L.csoc); gd* dsoc = A(L.dsoc);
           const gd* ct = A(L.ct); const gd* dtv = A(L.dt);
+          HTP_UNROLL
           for (int r = c.lane; r < D.mc; r += c.width) csoc[r] = alpha * cc[r] + ct[r];
+          HTP_UNROLL
           for (int r = c.lane; r < D.md; r += c.width) dsoc[r] = alpha * (dd[r] - s[r]) + (dtv[r] - st[r]);
           c.sync();
           double th_old = theta;
@@ -1965,19 +2097,26 @@ struct ObcaSolver {
           gd* ss_ = A(L.dvL); gd* syc = A(L.syc); gd* syd = A(L.syd);
           gd* nrc = A(L.ct); gd* nrd = A(L.dt);
           for (int k = 0; k < o.max_soc; ++k) {
+            HTP_UNROLL
             for (int r = c.lane; r < D.mc; r += c.width) nrc[r] = -csoc[r];
+            HTP_UNROLL
             for (int r = c.lane; r < D.md; r += c.width) nrd[r] = -dsoc[r];
             c.sync();
             kkt_solve(false, dw, dc, rxk, rs, nrc, nrd, sx, ss_, syc, syd);
             const double a_soc = frac_primal(sx, ss_);
+            HTP_UNROLL
             for (int q = c.lane; q < D.n; q += c.width) xt[q] = x[q] + a_soc * sx[q];
+            HTP_UNROLL
             for (int r = c.lane; r < D.md; r += c.width) st[r] = s[r] + a_soc * ss_[r];
             c.sync();
             double th_soc, ph_soc;
             if (acceptable(alpha, xt, st, phi, theta, gBD, is_ftype(alpha), th_soc, ph_soc)) {
-              accepted = true; soc_used = true; a_primal = a_soc; a_test = alpha; ph_t = ph_soc;
+              accepted = true; soc_used = true; a_primal = a_soc; a_test = alpha; ph_t = ph_soc; th_acc = th_soc;
+              HTP_UNROLL
               for (int q = c.lane; q < D.n; q += c.width) dx[q] = sx[q];
+              HTP_UNROLL
               for (int r = c.lane; r < D.md; r += c.width) { ds[r] = ss_[r]; dyd[r] = syd[r]; }
+              HTP_UNROLL
               for (int r = c.lane; r < D.mc; r += c.width) dyc[r] = syc[r];
               c.sync();
               break;
@@ -1985,7 +2124,9 @@ struct ObcaSolver {
             if (th_soc > o.kappa_soc * th_old) break;
             th_old = th_soc;
             const gd* ct2 = A(L.ct); const gd* dt2 = A(L.dt);
+            HTP_UNROLL
             for (int r = c.lane; r < D.mc; r += c.width) csoc[r] = a_soc * csoc[r] + ct2[r];
+            HTP_UNROLL
             for (int r = c.lane; r < D.md; r += c.width) dsoc[r] = a_soc * dsoc[r] + (dt2[r] - st[r]);
             c.sync();
           }
@@ -1994,6 +2135,7 @@ struct ObcaSolver {
         first = false;
         alpha *= 0.5;
       }
+      cyc[6] += c.clock() - tls;
       if (!accepted) { status = ST_RESTORATION; break; }
       (void)soc_used;
       // filter augmentation (uses the accepted trial's barrier value)
@@ -2007,6 +2149,7 @@ struct ObcaSolver {
         if (nfilt < FMAX) ++nfilt;
         c.sync();
       }
+      long long tup = c.clock();
       const double a_dual = dual_steps(dx, ds);
       {
         gd* zL = A(L.zL); gd* zU = A(L.zU); gd* vL = A(L.vL); gd* vU = A(L.vU);
@@ -2016,22 +2159,36 @@ struct ObcaSolver {
         const gd* xL = A(L.xL); const gd* xU = A(L.xU);
         const gd* dL = A(L.dL); const gd* dU = A(L.dU);
         const double ks = o.kappa_sigma;
+        HTP_UNROLL
         for (int q = c.lane; q < D.n; q += c.width) {
           x[q] += a_primal * dx[q];
           if (finite_(xL[q])) { const double z = zL[q] + a_dual * dzL[q], v = x[q] - xL[q]; zL[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
           if (finite_(xU[q])) { const double z = zU[q] + a_dual * dzU[q], v = xU[q] - x[q]; zU[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
         }
+        HTP_UNROLL
         for (int r = c.lane; r < D.md; r += c.width) {
           s[r] += a_primal * ds[r];
           yd[r] += a_primal * dyd[r];
           { const double z = vL[r] + a_dual * dvL[r], v = s[r] - dL[r]; vL[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
           if (finite_(dU[r])) { const double z = vU[r] + a_dual * dvU[r], v = dU[r] - s[r]; vU[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
         }
+        HTP_UNROLL
         for (int r = c.lane; r < D.mc; r += c.width) yc[r] += a_primal * dyc[r];
         c.sync();
       }
-      eval_cons(x, cc, dd);
+      {  // constraint values at the new point = those of the accepted trial point
+        const gd* ct = A(L.ct); const gd* dtv = A(L.dt);
+        HTP_UNROLL
+        for (int r = c.lane; r < D.mc; r += c.width) cc[r] = ct[r];
+        HTP_UNROLL
+        for (int r = c.lane; r < D.md; r += c.width) dd[r] = dtv[r];
+      }
+      phi_cache = ph_t;
+      mu_cache = mu;
+      theta_cache = th_acc;
+      c.sync();
       eval_grad_f(x, A(L.gf), sf);
+      cyc[7] += c.clock() - tup;
     }
     // honor_original_bounds: project into the unrelaxed bounds
     project_original_bounds();
@@ -2054,6 +2211,7 @@ struct ObcaSolver {
     const double vmax = dabs(par(P_MAXV)), smax = dabs(par(P_MAXSTEER));
     const double amax = dabs(par(P_MAXACC)), wmax = dabs(par(P_MAXSR));
     const double twopi = 2.0 * M_PI;
+    HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) {
       double lo = -HTP_INF, hi = HTP_INF;
       if (q < D.oU) {

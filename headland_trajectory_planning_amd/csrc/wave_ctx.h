@@ -17,27 +17,44 @@ struct DevWave {
   int lane;
   ld* lds;    // per-wave LDS scratch
   li* ildsp;  // per-wave LDS int scratch
-  __device__ __forceinline__ void sync() const { __syncthreads(); }
+  // The workgroup is a single wavefront: its LDS and global accesses are
+  // performed in program order, so cross-lane RAW only needs the compiler not
+  // to reorder memory operations -- a wavefront-scope fence (no s_waitcnt
+  // vmcnt(0), unlike __syncthreads(), so prefetches and stores stay in flight).
+  __device__ __forceinline__ void sync() const {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  // Reduction results are identical in every lane; readfirstlane tells the
+  // compiler so (scalar registers, uniform branches instead of exec masks).
+  __device__ __forceinline__ static double uni(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+  }
   __device__ __forceinline__ double sum(double v) const {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return uni(v);
   }
   __device__ __forceinline__ double maxv(double v) const {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
+    return uni(v);
   }
   __device__ __forceinline__ double minv(double v) const {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
+    return uni(v);
   }
   __device__ __forceinline__ int isum(int v) const {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return __builtin_amdgcn_readfirstlane(v);
   }
+  __device__ __forceinline__ double uniform(double v) const { return uni(v); }
+  __device__ __forceinline__ int uniform_i(int v) const { return __builtin_amdgcn_readfirstlane(v); }
   __device__ __forceinline__ double bcast(double v, int src) const { return __shfl(v, src, 64); }
   __device__ __forceinline__ long long clock() const { return (long long)__builtin_amdgcn_s_memtime(); }
 };
@@ -59,6 +76,8 @@ struct HostLane {
   double minv(double v) const { return v; }
   int isum(int v) const { return v; }
   double bcast(double v, int) const { return v; }
+  double uniform(double v) const { return v; }
+  int uniform_i(int v) const { return v; }
   long long clock() const { return 0; }
 };
 

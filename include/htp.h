@@ -90,8 +90,8 @@ int htp_obca_solve_batch_device(htp_ctx* ctx, const htp_obca_batch* in, htp_obca
 /* Average duration (ms) of the last solve kernel measured with hipEvents on
  * the launch stream (used by bench.py for the roofline). */
 double htp_last_kernel_ms(htp_ctx* ctx);
-/* Diagnostic: per-problem shader-cycle counters of the last solve, [batch][6]:
- * local-block sweeps, stage assembly, stage chain, KKT solves, total, reserved. */
+ /* Diagnostic: per-problem shader-cycle counters of the last solve, [batch][8]:
+ * local sweeps, assembly, stage chain, KKT solves, total, errors+grad_lag, line search, update. */
 int htp_last_cycles(htp_ctx* ctx, int64_t* out, int32_t batch);
 
 #ifdef __cplusplus

@@ -10,9 +10,10 @@ from headland_trajectory_planning_amd import _native, synth  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else "B"
 batch = int(sys.argv[2]) if len(sys.argv) > 2 else None
 b, N, M, imp = synth.CONFIGS[cfg]
+import bench
 batch = batch or b
 t = time.time()
-insts = [synth.make_instance(pid, N=N, M=M, implement=imp) for pid in range(batch)]
+insts = bench.make_batch(list(range(batch)), N, M, imp, 16)
 print(f"gen {batch} problems: {time.time() - t:.1f}s", flush=True)
 pk = _native.PackedBatch(insts)
 ctx = _native.Context(0)
@@ -26,6 +27,7 @@ print("status counts", np.bincount(res.status, minlength=6), "iters mean", res.i
       "p99", np.percentile(res.iterations, 99), "max", res.iterations.max(), "nfactor mean", res.n_factor.mean())
 cyc = ctx.last_cycles(batch).astype(float)
 tot = cyc[:, 4].sum()
-print("cycle share: local %.3f assemble %.3f stagechain %.3f kktsolve %.3f ; mean total cycles/problem %.3g, per iter %.3g" % (
-    cyc[:, 0].sum() / tot, cyc[:, 1].sum() / tot, cyc[:, 2].sum() / tot, cyc[:, 3].sum() / tot, cyc[:, 4].mean(),
-    (cyc[:, 4] / np.maximum(1, res.iterations)).mean()))
+names = ["local", "assemble", "chain", "kktsolve", "total", "errors", "linesearch", "update"]
+print("cycle share:", " ".join(f"{names[k]} {cyc[:, k].sum() / tot:.3f}" for k in (0, 1, 2, 3, 5, 6, 7)),
+      "| other %.3f" % (1 - sum(cyc[:, k].sum() for k in (0, 1, 2, 3, 5, 6, 7)) / tot),
+      "| per-iter cycles %.3g" % (cyc[:, 4] / np.maximum(1, res.iterations)).mean())
