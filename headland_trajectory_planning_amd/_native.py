@@ -34,8 +34,20 @@ class ObcaResult(ctypes.Structure):
                 ("iterations", ctypes.c_void_p), ("n_factor", ctypes.c_void_p), ("nlp_error", ctypes.c_void_p)]
 
 
+class RsPaths(ctypes.Structure):
+    _fields_ = [("cap_paths", ctypes.c_int64), ("cap_points", ctypes.c_int64), ("n_paths", ctypes.c_int64),
+                ("n_points", ctypes.c_int64)] + [(n, ctypes.c_void_p) for n in (
+                    "path_offsets", "status", "lengths", "ctypes", "L", "point_offsets", "x", "y", "yaw", "cs",
+                    "directions")]
+
+
+RS_OK, RS_ASSERT, RS_OVERFLOW, RS_CAPACITY = 0, 1, 2, 3
+RS_SEG = "LSR"  # HTP_RS_SEG_L / _S / _R
+
+
 EXPORTS = ["htp_obca_sizes", "htp_create", "htp_destroy", "htp_last_error", "htp_set_option",
-           "htp_obca_solve_batch", "htp_obca_solve_batch_device", "htp_last_kernel_ms", "htp_last_cycles"]
+           "htp_obca_solve_batch", "htp_obca_solve_batch_device", "htp_last_kernel_ms", "htp_last_cycles",
+           "htp_rs_all_paths_batch", "htp_rs_all_paths_batch_device", "htp_rs_last_ms"]
 
 
 def _declare(lib):
@@ -58,6 +70,13 @@ def _declare(lib):
     lib.htp_last_kernel_ms.restype = ctypes.c_double
     lib.htp_last_cycles.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
     lib.htp_last_cycles.restype = ctypes.c_int
+    lib.htp_rs_all_paths_batch.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.POINTER(RsPaths)]
+    lib.htp_rs_all_paths_batch.restype = ctypes.c_int
+    lib.htp_rs_all_paths_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                                  ctypes.POINTER(RsPaths), ctypes.c_void_p, ctypes.c_void_p]
+    lib.htp_rs_all_paths_batch_device.restype = ctypes.c_int
+    lib.htp_rs_last_ms.argtypes = [ctypes.c_void_p]
+    lib.htp_rs_last_ms.restype = ctypes.c_double
     return lib
 
 
@@ -71,6 +90,13 @@ def load(path=LIB_PATH):
         return _LIB
     if not os.path.exists(path):
         raise RuntimeError(f"[htp] HIP library not built: {path} (run __graft_entry__.build())")
+    # torch wheels bundle their own libamdhip64.so.7 (same SONAME as /opt/rocm's).
+    # Whichever is loaded first serves the whole process; loading torch's first
+    # keeps torch.cuda working when callers import torch after this library.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = _declare(ctypes.CDLL(path))
     if path == LIB_PATH:
         _LIB = lib
@@ -228,6 +254,43 @@ class Context:
         if self.lib.htp_last_cycles(self.ctx, out.ctypes.data, int(batch)) != 0:
             raise RuntimeError(self.error())
         return out
+
+    def rs_all_paths(self, queries):
+        """Reeds-Shepp calc_all_paths for a batch of queries [B, 8] =
+        (sx, sy, syaw, gx, gy, gyaw, maxc, step_size); returns CSR numpy arrays
+        (host buffers; a size query first, then the fill)."""
+        q = np.ascontiguousarray(np.asarray(queries, dtype=np.float64).reshape(-1, 8))
+        B = q.shape[0]
+        out = {"path_offsets": np.zeros(B + 1, np.int64), "status": np.zeros(B, np.int32)}
+        cap_p = cap_q = 0
+        for _ in range(2):
+            out.update(lengths=np.zeros((cap_p, 5)), ctypes=np.zeros((cap_p, 5), np.int8), L=np.zeros(cap_p),
+                       point_offsets=np.zeros(cap_p + 1, np.int64), x=np.zeros(cap_q), y=np.zeros(cap_q),
+                       yaw=np.zeros(cap_q), cs=np.zeros(cap_q), directions=np.zeros(cap_q, np.int8))
+            st = RsPaths(cap_p, cap_q, 0, 0, *[out[k].ctypes.data for k in (
+                "path_offsets", "status", "lengths", "ctypes", "L", "point_offsets", "x", "y", "yaw", "cs",
+                "directions")])
+            rc = self.lib.htp_rs_all_paths_batch(self.ctx, B, q.ctypes.data, ctypes.byref(st))
+            if rc == 0:
+                break
+            if rc != RS_CAPACITY:
+                raise RuntimeError(f"[htp] htp_rs_all_paths_batch failed: {self.error()}")
+            cap_p, cap_q = int(st.n_paths), int(st.n_points)
+        else:
+            raise RuntimeError("[htp] htp_rs_all_paths_batch: capacity negotiation failed")
+        out["n_paths"], out["n_points"] = int(st.n_paths), int(st.n_points)
+        return out
+
+    def rs_all_paths_device(self, batch, q_ptr, out_ptrs, caps, totals_ptr, stream=None):
+        st = RsPaths(int(caps[0]), int(caps[1]), 0, 0, *[out_ptrs.get(k) for k in (
+            "path_offsets", "status", "lengths", "ctypes", "L", "point_offsets", "x", "y", "yaw", "cs",
+            "directions")])
+        rc = self.lib.htp_rs_all_paths_batch_device(self.ctx, int(batch), q_ptr, ctypes.byref(st), totals_ptr, stream)
+        if rc != 0:
+            raise RuntimeError(f"[htp] htp_rs_all_paths_batch_device failed: {self.error()}")
+
+    def rs_last_ms(self):
+        return self.lib.htp_rs_last_ms(self.ctx)
 
     def close(self):
         if self.ctx:

@@ -1,0 +1,48 @@
+// Library context shared by the translation units of libhtp.so (host side).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "htp_common.h"
+
+struct htp_ctx {
+  using Options = htp::Options;
+  using Shape = htp::Shape;
+  int device = 0;
+  std::string err;
+  Options opt = htp::default_options();
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  void* scratch = nullptr;  // Result array
+  size_t scratch_bytes = 0;
+  Shape* shape = nullptr;   // device copy of the launch-uniform shape
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double last_ms = 0.0;
+  // Reeds-Shepp batch (htp_rs.hip)
+  void* rs_scratch = nullptr;
+  size_t rs_scratch_bytes = 0;
+  hipEvent_t rs_ev0 = nullptr, rs_ev1 = nullptr;
+};
+
+static inline int fail(htp_ctx* c, const std::string& m) {
+  if (c) c->err = m;
+  return -1;
+}
+
+#define HIPCHK(expr)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess) return fail(ctx, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+static inline int ensure(htp_ctx* ctx, void** p, size_t* have, size_t need) {
+  if (*have >= need) return 0;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  HIPCHK(hipMalloc(p, need));
+  *have = need;
+  return 0;
+}
+

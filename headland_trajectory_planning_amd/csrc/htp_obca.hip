@@ -63,39 +63,7 @@ __global__ void unpack_results(const Result* __restrict__ r, int batch, double* 
 
 }  // namespace
 
-struct htp_ctx {
-  int device = 0;
-  std::string err;
-  Options opt = default_options();
-  void* ws = nullptr;
-  size_t ws_bytes = 0;
-  void* scratch = nullptr;  // Result array
-  size_t scratch_bytes = 0;
-  Shape* shape = nullptr;   // device copy of the launch-uniform shape
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  double last_ms = 0.0;
-};
-
-static int fail(htp_ctx* c, const std::string& m) {
-  if (c) c->err = m;
-  return -1;
-}
-
-#define HIPCHK(expr)                                                                 \
-  do {                                                                               \
-    hipError_t e_ = (expr);                                                          \
-    if (e_ != hipSuccess) return fail(ctx, std::string(#expr ": ") + hipGetErrorString(e_)); \
-  } while (0)
-
-static int ensure(htp_ctx* ctx, void** p, size_t* have, size_t need) {
-  if (*have >= need) return 0;
-  if (*p) (void)hipFree(*p);
-  *p = nullptr;
-  *have = 0;
-  HIPCHK(hipMalloc(p, need));
-  *have = need;
-  return 0;
-}
+#include "htp_ctx.h"
 
 extern "C" {
 
@@ -121,6 +89,8 @@ htp_ctx* htp_create(int32_t device) {
   }
   (void)hipEventCreate(&c->ev0);
   (void)hipEventCreate(&c->ev1);
+  (void)hipEventCreate(&c->rs_ev0);
+  (void)hipEventCreate(&c->rs_ev1);
   return c;
 }
 
@@ -131,6 +101,9 @@ void htp_destroy(htp_ctx* c) {
   if (c->shape) (void)hipFree(c->shape);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->rs_scratch) (void)hipFree(c->rs_scratch);
+  if (c->rs_ev0) (void)hipEventDestroy(c->rs_ev0);
+  if (c->rs_ev1) (void)hipEventDestroy(c->rs_ev1);
   delete c;
 }
 

@@ -94,6 +94,48 @@ double htp_last_kernel_ms(htp_ctx* ctx);
  * local sweeps, assembly, stage chain, KKT solves, total, errors+grad_lag, line search, update. */
 int htp_last_cycles(htp_ctx* ctx, int64_t* out, int32_t batch);
 
+/* ---------------------------------------------------------------------------
+ * Reeds-Shepp: all admissible paths between pose pairs, sampled
+ * (R/path_planner/utils/reeds_shepp.py calc_all_paths :39-65, called by
+ * hybrid_a_star_search.py:248 and safety_forward_path_plan.py:368).
+ * Query q = (sx, sy, syaw, gx, gy, gyaw, maxc, step_size).  Output is CSR:
+ * paths of query q are [path_offsets[q], path_offsets[q+1]); samples of path p
+ * are [point_offsets[p], point_offsets[p+1]).  Path order, lengths, ctypes,
+ * sample count and values follow the reference (de-duplication, MAX_LENGTH
+ * filter and trailing-zero pop included). */
+enum { HTP_RS_SEG_L = 0, HTP_RS_SEG_S = 1, HTP_RS_SEG_R = 2, HTP_RS_SEG_NONE = 3 };
+enum {
+  HTP_RS_OK = 0,
+  HTP_RS_ASSERT = 1,      /* reference raises AssertionError (a path with L < 0.01); no paths returned */
+  HTP_RS_OVERFLOW = 2,    /* reference raises IndexError in generate_local_course; no paths returned */
+  HTP_RS_CAPACITY = 3     /* return code only: output capacity too small, totals reported */
+};
+
+typedef struct {
+  int64_t cap_paths, cap_points;  /* in: capacity of the arrays below */
+  int64_t n_paths, n_points;      /* out: totals needed/written */
+  int64_t* path_offsets;          /* [batch+1] */
+  int32_t* status;                /* [batch] HTP_RS_* */
+  double* lengths;                /* [cap_paths][5] PATH.lengths (unused entries 0) */
+  int8_t* ctypes;                 /* [cap_paths][5] HTP_RS_SEG_* */
+  double* L;                      /* [cap_paths] PATH.L */
+  int64_t* point_offsets;         /* [cap_paths+1] */
+  double *x, *y, *yaw, *cs;       /* [cap_points] PATH.x/.y/.yaw/.cs */
+  int8_t* directions;             /* [cap_points] PATH.directions */
+} htp_rs_paths;
+
+/* Host buffers (synchronous).  Returns HTP_RS_CAPACITY with n_paths/n_points
+ * (and status) filled when a capacity is too small; call again with larger
+ * arrays (caps 0 = size query). */
+int htp_rs_all_paths_batch(htp_ctx* ctx, int32_t batch, const double* queries, htp_rs_paths* out);
+/* Device buffers, enqueued on `stream`.  `totals` (device int64[2]) receives
+ * (n_paths, n_points); arrays are written only where they fit the capacities
+ * (points beyond cap_points and paths beyond cap_paths are skipped). */
+int htp_rs_all_paths_batch_device(htp_ctx* ctx, int32_t batch, const double* queries, htp_rs_paths* out,
+                                  int64_t* totals, void* stream);
+/* Duration (ms) of the last RS batch (hipEvents around its kernels). */
+double htp_rs_last_ms(htp_ctx* ctx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,8 +20,8 @@ def build():
     srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
     if os.path.exists(SO) and os.path.getmtime(SO) >= max(os.path.getmtime(s) for s in srcs):
         return SO
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", SO,
-                           os.path.join(CSRC, "htp_hostsim.cpp")])
+    subprocess.check_call(["g++", "-O2", "-fno-builtin", "-std=c++17", "-shared", "-fPIC", "-o", SO,
+                           os.path.join(CSRC, "htp_hostsim.cpp"), os.path.join(CSRC, "rs_hostsim.cpp")])
     return SO
 
 
@@ -70,3 +70,40 @@ def solve_threadsim(insts, max_iter=-1):
     rc = lib_.htp_threadsim_obca_solve(ctypes.byref(pk.struct()), ctypes.byref(res.struct()), max_iter)
     assert rc == 0
     return res
+
+
+def rs_host(queries):
+    """Host build of csrc/rs_core.h (same CSR dict as Context.rs_all_paths),
+    one query per call.  TEST-ONLY."""
+    l = lib()
+    f = l.htp_hostsim_rs
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 11
+    q = np.ascontiguousarray(np.asarray(queries, dtype=np.float64).reshape(-1, 8))
+    parts = {k: [] for k in ("lengths", "ctypes", "L", "x", "y", "yaw", "cs", "directions")}
+    status, npaths, npts_path = [], [], []
+    np1, nq = np.zeros(1, np.int32), np.zeros(1, np.int64)
+    for row in q:
+        cp, cq = 0, 0
+        for _ in range(2):
+            ln, ct, L = np.zeros((cp, 5)), np.zeros((cp, 5), np.int8), np.zeros(cp)
+            off = np.zeros(cp + 1, np.int64)
+            x, y, yaw, cs = (np.zeros(cq) for _ in range(4))
+            d = np.zeros(cq, np.int8)
+            st = f(row.ctypes.data, cp, cq, np1.ctypes.data, nq.ctypes.data, ln.ctypes.data, ct.ctypes.data,
+                   L.ctypes.data, off.ctypes.data, x.ctypes.data, y.ctypes.data, yaw.ctypes.data, cs.ctypes.data,
+                   d.ctypes.data)
+            if cp >= np1[0] and cq >= nq[0]:
+                break
+            cp, cq = int(np1[0]), int(nq[0])
+        status.append(st)
+        npaths.append(int(np1[0]))
+        npts_path.extend(np.diff(off).tolist())
+        for k, v in zip(("lengths", "ctypes", "L", "x", "y", "yaw", "cs", "directions"), (ln, ct, L, x, y, yaw, cs, d)):
+            parts[k].append(v)
+    out = {k: np.concatenate(v) if v else np.zeros(0) for k, v in parts.items()}
+    out["status"] = np.array(status, np.int32)
+    out["path_offsets"] = np.concatenate([[0], np.cumsum(npaths)]).astype(np.int64)
+    out["point_offsets"] = np.concatenate([[0], np.cumsum(npts_path)]).astype(np.int64)
+    out["n_paths"], out["n_points"] = int(out["path_offsets"][-1]), int(out["point_offsets"][-1])
+    return out
