@@ -41,13 +41,33 @@ class RsPaths(ctypes.Structure):
                     "directions")]
 
 
+class HaBatch(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("batch", "npoly", "nvert", "nguide", "nmotion")] + \
+        [(n, ctypes.c_void_p) for n in ("params", "desc", "poly_off", "vertices", "lane_len", "guide", "motions")] + \
+        [(n, ctypes.c_int32) for n in ("max_nodes_cap", "cap_path", "cap_log")]
+
+
+class HaResult(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("status", "counter", "n_path", "n_expanded", "n_pose", "x", "y", "yaw",
+                                               "dir", "k", "expanded")]
+
+
+HA_NPARAM, HA_NDESC = 16, 12
+(HA_P_SX, HA_P_SY, HA_P_SYAW, HA_P_GX, HA_P_GY, HA_P_GYAW, HA_P_RES, HA_P_YAWRES, HA_P_WB, HA_P_MAXSTEER,
+ HA_P_CURV, HA_P_DEFLEN, HA_P_MAXNODES) = range(13)
+(HA_D_BODY, HA_D_BLK0, HA_D_BLK1, HA_D_LANE0, HA_D_LANE1, HA_D_FIELD, HA_D_GUIDE0, HA_D_GUIDE1, HA_D_MOT0,
+ HA_D_MOT1, HA_D_KING) = range(11)
+HA_STATUS = {0: "found", 1: "no_path", 2: "max_nodes", 3: "start_goal_blocked", 4: "rs_error", 5: "capacity",
+             6: "bad_input", 7: "backtrack_error"}
+
 RS_OK, RS_ASSERT, RS_OVERFLOW, RS_CAPACITY = 0, 1, 2, 3
 RS_SEG = "LSR"  # HTP_RS_SEG_L / _S / _R
 
 
 EXPORTS = ["htp_obca_sizes", "htp_create", "htp_destroy", "htp_last_error", "htp_set_option",
            "htp_obca_solve_batch", "htp_obca_solve_batch_device", "htp_last_kernel_ms", "htp_last_cycles",
-           "htp_rs_all_paths_batch", "htp_rs_all_paths_batch_device", "htp_rs_last_ms"]
+           "htp_rs_all_paths_batch", "htp_rs_all_paths_batch_device", "htp_rs_last_ms",
+           "htp_hastar_search_batch", "htp_hastar_search_batch_device", "htp_hastar_last_ms"]
 
 
 def _declare(lib):
@@ -77,6 +97,13 @@ def _declare(lib):
     lib.htp_rs_all_paths_batch_device.restype = ctypes.c_int
     lib.htp_rs_last_ms.argtypes = [ctypes.c_void_p]
     lib.htp_rs_last_ms.restype = ctypes.c_double
+    lib.htp_hastar_search_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaBatch), ctypes.POINTER(HaResult)]
+    lib.htp_hastar_search_batch.restype = ctypes.c_int
+    lib.htp_hastar_search_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaBatch), ctypes.POINTER(HaResult),
+                                                   ctypes.c_void_p]
+    lib.htp_hastar_search_batch_device.restype = ctypes.c_int
+    lib.htp_hastar_last_ms.argtypes = [ctypes.c_void_p]
+    lib.htp_hastar_last_ms.restype = ctypes.c_double
     return lib
 
 
@@ -209,6 +236,122 @@ class HostResults:
         return r
 
 
+def _clean_ring(poly):
+    """Vertices without the repeated closing vertex or consecutive duplicates."""
+    a = np.asarray(poly, dtype=np.float64).reshape(-1, 2)
+    keep = [0]
+    for i in range(1, a.shape[0]):
+        if not np.array_equal(a[i], a[keep[-1]]):
+            keep.append(i)
+    a = a[keep]
+    if a.shape[0] > 1 and np.array_equal(a[0], a[-1]):
+        a = a[:-1]
+    return a
+
+
+def _ccw(a):
+    area = np.sum(a[:, 0] * np.roll(a[:, 1], -1) - np.roll(a[:, 0], -1) * a[:, 1])
+    return a if area > 0 else a[::-1].copy()
+
+
+class HastarPacked:
+    """htp_hastar_batch pools for a list of lowered hybrid A* problems (dicts
+    made by path_planner.hybrid_a_star_search.lower_problem)."""
+
+    def __init__(self, probs, cap_path=4096, cap_log=None):
+        B = len(probs)
+        polys, lane_len, guides, motions = [], [], [], []
+        self.params = np.zeros((B, HA_NPARAM))
+        self.desc = np.zeros((B, HA_NDESC), dtype=np.int32)
+        ng = nm = 0
+        for b, p in enumerate(probs):
+            if not p.get("king", True):
+                raise NotImplementedError("[HA*] motion_type 'Pawn' (Dubins goal shots) is not supported by the kernel")
+            d = self.desc[b]
+            d[HA_D_BODY] = len(polys)
+            polys.append(_clean_ring(p["body"]))
+            lane_len.append(0.0)
+            d[HA_D_BLK0] = len(polys)
+            for q in p["blockers"]:
+                polys.append(_clean_ring(q))
+                lane_len.append(0.0)
+            d[HA_D_BLK1] = len(polys)
+            d[HA_D_LANE0] = len(polys)
+            for q, L in zip(p["lanes"], p["search_lengths"]):
+                polys.append(_ccw(_clean_ring(q)))
+                lane_len.append(float(L))
+            d[HA_D_LANE1] = len(polys)
+            if p["field"] is None:
+                d[HA_D_FIELD] = -1
+            else:
+                d[HA_D_FIELD] = len(polys)
+                polys.append(_clean_ring(p["field"]))
+                lane_len.append(0.0)
+            g = np.asarray(p["guide"], dtype=np.float64).reshape(-1, 4)
+            d[HA_D_GUIDE0], d[HA_D_GUIDE1] = ng, ng + g.shape[0]
+            guides.append(g)
+            ng += g.shape[0]
+            m = np.asarray(p["motions"], dtype=np.float64).reshape(-1, 2)
+            d[HA_D_MOT0], d[HA_D_MOT1] = nm, nm + m.shape[0]
+            motions.append(m)
+            nm += m.shape[0]
+            d[HA_D_KING] = 1
+            pr = self.params[b]
+            pr[HA_P_SX:HA_P_SYAW + 1] = np.asarray(p["start"], dtype=np.float64)[:3]
+            pr[HA_P_GX:HA_P_GYAW + 1] = np.asarray(p["goal"], dtype=np.float64)[:3]
+            pr[HA_P_RES], pr[HA_P_YAWRES] = p["res"], p["yaw_res"]
+            pr[HA_P_WB], pr[HA_P_MAXSTEER], pr[HA_P_CURV] = p["wheel_base"], p["max_steer"], p["curvature"]
+            pr[HA_P_DEFLEN], pr[HA_P_MAXNODES] = p["default_search_length"], p["max_nodes"]
+        self.batch = B
+        self.poly_off = np.zeros(len(polys) + 1, dtype=np.int32)
+        self.poly_off[1:] = np.cumsum([q.shape[0] for q in polys])
+        self.vertices = np.ascontiguousarray(np.concatenate(polys, axis=0))
+        self.lane_len = np.array(lane_len, dtype=np.float64)
+        self.guide = np.ascontiguousarray(np.concatenate(guides, axis=0))
+        self.motions = np.ascontiguousarray(np.concatenate(motions, axis=0))
+        self.max_nodes_cap = int(max(int(p["max_nodes"]) for p in probs)) if B else 0
+        self.cap_path = int(cap_path)
+        self.cap_log = int(self.max_nodes_cap + 2 if cap_log is None else cap_log)
+
+    def struct(self, ptrs=None):
+        src = ptrs or {}
+        b = HaBatch()
+        b.batch, b.npoly, b.nvert = self.batch, len(self.poly_off) - 1, self.vertices.shape[0]
+        b.nguide, b.nmotion = self.guide.shape[0], self.motions.shape[0]
+        for n in ("params", "desc", "poly_off", "vertices", "lane_len", "guide", "motions"):
+            setattr(b, n, src[n] if n in src else getattr(self, n).ctypes.data)
+        b.max_nodes_cap, b.cap_path, b.cap_log = self.max_nodes_cap, self.cap_path, self.cap_log
+        return b
+
+
+class HastarResults:
+    def __init__(self, packed):
+        B, cp, cl = packed.batch, packed.cap_path, packed.cap_log
+        self.status = np.zeros(B, np.int32)
+        self.counter = np.zeros(B, np.int32)
+        self.n_path = np.zeros(B, np.int32)
+        self.n_expanded = np.zeros(B, np.int32)
+        self.n_pose = np.zeros(B, np.int64)
+        for n in ("x", "y", "yaw", "dir", "k"):
+            setattr(self, n, np.zeros((B, cp)))
+        self.expanded = np.zeros((B, cl, 3), np.int32)
+
+    def struct(self):
+        r = HaResult()
+        for n in ("status", "counter", "n_path", "n_expanded", "n_pose", "x", "y", "yaw", "dir", "k", "expanded"):
+            setattr(r, n, getattr(self, n).ctypes.data)
+        return r
+
+    def path(self, b):
+        """(xs, ys, yaws, dirs, ks) of search b as lists (truncated to cap_path)."""
+        n = min(int(self.n_path[b]), self.x.shape[1])
+        return tuple(getattr(self, k)[b, :n].tolist() for k in ("x", "y", "yaw", "dir", "k"))
+
+    def expansions(self, b):
+        n = min(int(self.n_expanded[b]), self.expanded.shape[1])
+        return [tuple(int(v) for v in r) for r in self.expanded[b, :n]]
+
+
 class Context:
     """Owns one htp_ctx (device workspace)."""
 
@@ -291,6 +434,27 @@ class Context:
 
     def rs_last_ms(self):
         return self.lib.htp_rs_last_ms(self.ctx)
+
+    def hastar(self, packed):
+        """Hybrid A* searches of a HastarPacked batch (host buffers, synchronous)."""
+        res = HastarResults(packed)
+        b, r = packed.struct(), res.struct()
+        rc = self.lib.htp_hastar_search_batch(self.ctx, ctypes.byref(b), ctypes.byref(r))
+        if rc != 0:
+            raise RuntimeError(f"[htp] htp_hastar_search_batch failed: {self.error()}")
+        return res
+
+    def hastar_device(self, packed, dev_ptrs, out_ptrs, stream=None):
+        b = packed.struct(dev_ptrs)
+        r = HaResult()
+        for k, v in out_ptrs.items():
+            setattr(r, k, v)
+        rc = self.lib.htp_hastar_search_batch_device(self.ctx, ctypes.byref(b), ctypes.byref(r), stream)
+        if rc != 0:
+            raise RuntimeError(f"[htp] htp_hastar_search_batch_device failed: {self.error()}")
+
+    def hastar_last_ms(self):
+        return self.lib.htp_hastar_last_ms(self.ctx)
 
     def close(self):
         if self.ctx:

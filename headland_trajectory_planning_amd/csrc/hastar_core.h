@@ -1,0 +1,909 @@
+// Hybrid A* warm-start search, one search per 64-lane wavefront.
+//
+// Behaviour of R/path_planner/hybrid_a_star_search.py (HybridAStarSearch with
+// motion_type="King": Reeds-Shepp goal shots) over lowered geometry:
+//   * open/closed dicts keyed by the grid index (calculate_node_index :82-89,
+//     Python round = half-to-even = rint) -> one open-addressing table whose
+//     slots carry the state (open / closed), the node and the heap position;
+//   * heapdict 1.0.1 priority queue (:504-596, value max(g, 50 h)) restated
+//     exactly (delete = unconditional bubble to the root + popitem; sift-up
+//     while parent >= child; sift-down with strict <), so ties pop in the
+//     reference's order;
+//   * goal extension (:232-287): all Reeds-Shepp words current -> goal
+//     (rs_core.h; the 46 candidate words are evaluated one per lane, then
+//     de-duplicated in reference order), costed by
+//     calculate_reeds_shepp_path_cost (:129-160, quirks kept), ordered by a
+//     second heapdict, each sampled path streamed through the collision test
+//     64 samples at a time with early exit;
+//   * motion expansion (:357-410): one lane per motion primitive integrates
+//     the numpy linspace / angle_wrap / cumsum trajectory sequentially (same
+//     rounding as numpy), then all lanes test the (motion, pose) pairs;
+//   * collision (:412-427): body polygon at every pose vs blocker polygons
+//     (separating axes), inside the field polygon, inside the union of the
+//     heuristic's lane polygons (edge coverage by clip intervals);
+//   * heuristic (reference_line_heuristic.py:120-158): search length from the
+//     last lane polygon that strictly contains the pose, wave argmin over the
+//     guide samples (first index on ties, like np.argmin).
+// Arithmetic follows the reference's expression order; no FMA contraction.
+#pragma once
+#include <cmath>
+#include <cstdint>
+
+#include "rs_core.h"
+
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+
+namespace htp {
+namespace ha {
+
+constexpr int MAXB = 8;       // body polygon vertices
+constexpr int MAXMOT = 16;    // motion primitives (King: 14, Pawn: 8)
+constexpr int MAXTRAJ = 64;   // poses per motion primitive (round(L/res) + 1)
+constexpr int MAXJ = 32;      // lane polygons
+constexpr int MAXCHAIN = 1 << 20;
+constexpr double PI = 3.141592653589793;
+
+// per-search double parameters (htp.h HTP_HA_P_*)
+enum {
+  P_SX, P_SY, P_SYAW, P_GX, P_GY, P_GYAW, P_RES, P_YAWRES, P_WB, P_MAXSTEER, P_CURV, P_DEFLEN, P_MAXNODES,
+  P_NP = 16
+};
+// per-search int descriptor (htp.h HTP_HA_D_*)
+enum {
+  D_BODY, D_BLK0, D_BLK1, D_LANE0, D_LANE1, D_FIELD, D_GUIDE0, D_GUIDE1, D_MOT0, D_MOT1, D_KING,
+  D_NDESC = 12
+};
+// search status (htp.h HTP_HA_*)
+enum { ST_FOUND = 0, ST_NO_PATH = 1, ST_MAX_NODES = 2, ST_START_GOAL_BLOCKED = 3, ST_RS_ERROR = 4,
+       ST_CAPACITY = 5, ST_BAD_INPUT = 6, ST_BACKTRACK = 7 };
+
+struct Geo {
+  const int32_t* poly_off;  // [npoly+1] vertex ranges
+  const double* vert;       // [nvert][2]
+  const double* lane_len;   // [npoly] search length of lane polygons
+  const double* guide;      // [nguide][4] x, y, yaw, s
+  const double* motion;     // [nmotion][2] steer, direction
+};
+
+struct Node {  // 64 B
+  double x, y, yaw, cost, curv;
+  int32_t kx, ky, kt;       // grid index
+  int32_t pkx, pky, pkt;    // parent grid index
+  int32_t parent;           // node id of the expanding node (-1: start)
+  int16_t kind;             // 0 start, 1 motion, 2 Reeds-Shepp goal shot
+  int16_t aux;              // motion index / RS path index
+  int32_t dir;
+};
+
+struct Slot {  // 24 B
+  int32_t kx, ky, kt;
+  int32_t state;  // 0 empty, 1 open, 2 closed
+  int32_t node;
+  int32_t hpos;
+};
+
+struct Work {  // per-search HBM workspace
+  Node* node;
+  Slot* slot;
+  double* hval;
+  int32_t* hslot;
+  int32_t cap_node, cap_slot;  // cap_slot: power of two
+};
+
+struct Out {
+  int32_t status, counter, n_path, n_expanded;
+  int64_t n_pose, n_checks;
+};
+
+// Wave-shared scratch (LDS on the device).
+struct Shared {
+  double body[MAXB * 2];
+  double traj[MAXMOT * MAXTRAJ * 3];
+  int32_t hit[MAXMOT];
+  double ccost[MAXMOT];
+  double ccurv[MAXMOT];
+  int32_t ckey[MAXMOT * 3];
+  // Reeds-Shepp
+  rs::Path paths[rs::MAXP];
+  double cand_len[rs::MAXP * 5];
+  int32_t cand_n[rs::MAXP];
+  double rval[rs::MAXP];
+  int32_t rkey[rs::MAXP];
+  int32_t rpos[rs::MAXP];
+  double pd[64];
+  int32_t pseg[64];
+  double org[6 * 3];
+  int32_t flag[2];
+  double red_d[64];
+  int32_t red_i[64];
+};
+
+HTP_HD inline double pymod(double x, double y) { return rs::pymod(x, y); }
+HTP_HD inline double angle_wrap(double a) { return pymod(a + PI, 2.0 * PI) - PI; }  // path_utils.angle_wrap
+
+template <class C>
+struct Search {
+  C& c;
+  const double* prm;
+  const int32_t* dsc;
+  Geo g;
+  Work w;
+  Shared& sh;
+  int nb, nmot;
+  double res, yaw_res, wb, curv_max, maxsteer;
+
+  HTP_HD Search(C& c_, const double* p, const int32_t* d, const Geo& g_, const Work& w_, Shared& s)
+      : c(c_), prm(p), dsc(d), g(g_), w(w_), sh(s) {
+    res = prm[P_RES];
+    yaw_res = prm[P_YAWRES];
+    wb = prm[P_WB];
+    curv_max = prm[P_CURV];
+    maxsteer = prm[P_MAXSTEER];
+    nmot = dsc[D_MOT1] - dsc[D_MOT0];
+    const int b0 = g.poly_off[dsc[D_BODY]];
+    nb = g.poly_off[dsc[D_BODY] + 1] - b0;
+    for (int q = c.lane; q < 2 * nb; q += C::width) sh.body[q] = g.vert[2 * b0 + q];
+    c.sync();
+  }
+
+  // ------------------------------------------------------------ reductions
+  HTP_HD int any(int v) const { return c.isum(v ? 1 : 0) > 0; }
+  // (value, index) min with the smallest index on ties; result uniform.
+  HTP_HD void argmin(double& v, int& i) const {
+    if (C::width == 1) return;
+    sh.red_d[c.lane] = v;
+    sh.red_i[c.lane] = i;
+    c.sync();
+    double bv = sh.red_d[0];
+    int bi = sh.red_i[0];
+    for (int l = 1; l < C::width; ++l) {
+      const double ov = sh.red_d[l];
+      const int oi = sh.red_i[l];
+      if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    c.sync();
+    v = bv;
+    i = bi;
+  }
+
+  // ------------------------------------------------------------ geometry
+  HTP_HD bool sat_hit(const double* bx, const double* by, int p) const {
+    const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
+    const double* V = g.vert + 2 * o;
+    for (int k = 0; k < nb; ++k) {  // body edges
+      const int k1 = (k + 1) == nb ? 0 : k + 1;
+      const double ex = bx[k1] - bx[k], ey = by[k1] - by[k];
+      const double nx = ey, ny = -ex;
+      double amin = 0, amax = 0, qmin = 0, qmax = 0;
+      for (int j = 0; j < nb; ++j) {
+        const double d = bx[j] * nx + by[j] * ny;
+        if (j == 0 || d < amin) amin = d;
+        if (j == 0 || d > amax) amax = d;
+      }
+      for (int j = 0; j < m; ++j) {
+        const double d = V[2 * j] * nx + V[2 * j + 1] * ny;
+        if (j == 0 || d < qmin) qmin = d;
+        if (j == 0 || d > qmax) qmax = d;
+      }
+      if (amax < qmin || qmax < amin) return false;
+    }
+    for (int k = 0; k < m; ++k) {  // blocker edges
+      const int k1 = (k + 1) == m ? 0 : k + 1;
+      const double ex = V[2 * k1] - V[2 * k], ey = V[2 * k1 + 1] - V[2 * k + 1];
+      const double nx = ey, ny = -ex;
+      double amin = 0, amax = 0, qmin = 0, qmax = 0;
+      for (int j = 0; j < nb; ++j) {
+        const double d = bx[j] * nx + by[j] * ny;
+        if (j == 0 || d < amin) amin = d;
+        if (j == 0 || d > amax) amax = d;
+      }
+      for (int j = 0; j < m; ++j) {
+        const double d = V[2 * j] * nx + V[2 * j + 1] * ny;
+        if (j == 0 || d < qmin) qmin = d;
+        if (j == 0 || d > qmax) qmax = d;
+      }
+      if (amax < qmin || qmax < amin) return false;
+    }
+    return true;
+  }
+
+  HTP_HD bool in_field(const double* bx, const double* by, int p) const {
+    const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
+    const double* V = g.vert + 2 * o;
+    for (int k = 0; k < nb; ++k) {  // crossing number of each corner
+      const double X = bx[k], Y = by[k];
+      bool inside = false;
+      for (int i = 0; i < m; ++i) {
+        const int j = (i + 1) == m ? 0 : i + 1;
+        const double xi = V[2 * i], yi = V[2 * i + 1], xj = V[2 * j], yj = V[2 * j + 1];
+        if ((yi > Y) != (yj > Y)) {
+          const double xc = (xj - xi) * (Y - yi) / (yj - yi) + xi;
+          if (X < xc) inside = !inside;
+        }
+      }
+      if (!inside) return false;
+    }
+    for (int k = 0; k < nb; ++k) {  // no proper crossing of body and field edges
+      const int k1 = (k + 1) == nb ? 0 : k + 1;
+      const double ax = bx[k], ay = by[k], bbx = bx[k1], bby = by[k1];
+      for (int i = 0; i < m; ++i) {
+        const int j = (i + 1) == m ? 0 : i + 1;
+        const double cx = V[2 * i], cy = V[2 * i + 1], dx = V[2 * j], dy = V[2 * j + 1];
+        const double o1 = (bbx - ax) * (cy - ay) - (bby - ay) * (cx - ax);
+        const double o2 = (bbx - ax) * (dy - ay) - (bby - ay) * (dx - ax);
+        const double o3 = (dx - cx) * (ay - cy) - (dy - cy) * (ax - cx);
+        const double o4 = (dx - cx) * (bby - cy) - (dy - cy) * (bbx - cx);
+        if (o1 * o2 < 0 && o3 * o4 < 0) return false;
+      }
+    }
+    return true;
+  }
+
+  // every body edge covered by the union of the lane polygons (CCW, convex)
+  HTP_HD bool in_lanes(const double* bx, const double* by) const {
+    const int j0 = dsc[D_LANE0], j1 = dsc[D_LANE1];
+    for (int k = 0; k < nb; ++k) {
+      const int k1 = (k + 1) == nb ? 0 : k + 1;
+      const double Ax = bx[k], Ay = by[k], Bx = bx[k1], By = by[k1];
+      double lo[MAXJ], hi[MAXJ];
+      int n = 0;
+      for (int p = j0; p < j1; ++p) {
+        const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
+        const double* V = g.vert + 2 * o;
+        double l = 0.0, h = 1.0;
+        bool dead = false;
+        for (int i = 0; i < m; ++i) {
+          const int j = (i + 1) == m ? 0 : i + 1;
+          const double vx = V[2 * i], vy = V[2 * i + 1];
+          const double ex = V[2 * j] - vx, ey = V[2 * j + 1] - vy;
+          const double c0 = ex * (Ay - vy) - ey * (Ax - vx);
+          const double c1 = ex * (By - Ay) - ey * (Bx - Ax);
+          if (c1 > 0) { const double t = -c0 / c1; if (t > l) l = t; }
+          else if (c1 < 0) { const double t = -c0 / c1; if (t < h) h = t; }
+          else if (c0 < 0) dead = true;
+        }
+        if (!dead && l <= h) { lo[n] = l; hi[n] = h; ++n; }
+      }
+      // == sorted sweep "no gap, reach >= 1" (intervals lie in [0, 1])
+      double reach = 0.0;
+      bool grew = true;
+      while (grew) {
+        grew = false;
+        for (int i = 0; i < n; ++i) {
+          if (lo[i] <= reach) {
+            if (hi[i] > reach) reach = hi[i];
+            lo[i] = 2.0;  // consumed
+            grew = true;
+          }
+        }
+      }
+      if (!(reach >= 1.0)) return false;
+    }
+    return true;
+  }
+
+  HTP_HD bool pose_hits(double x, double y, double yaw) const {
+    const double cs = cos(yaw), sn = sin(yaw);
+    double bx[MAXB], by[MAXB];
+    for (int k = 0; k < nb; ++k) {
+      const double vx = sh.body[2 * k], vy = sh.body[2 * k + 1];
+      bx[k] = cs * vx + (-sn) * vy + x;
+      by[k] = sn * vx + cs * vy + y;
+    }
+    for (int p = dsc[D_BLK0]; p < dsc[D_BLK1]; ++p)
+      if (sat_hit(bx, by, p)) return true;
+    if (dsc[D_FIELD] >= 0 && !in_field(bx, by, dsc[D_FIELD])) return true;
+    if (!in_lanes(bx, by)) return true;
+    return false;
+  }
+
+  // ------------------------------------------------------------ heuristic
+  HTP_HD double search_length(double x, double y) const {  // get_search_length :120-129
+    double out = prm[P_DEFLEN];
+    for (int p = dsc[D_LANE0]; p < dsc[D_LANE1]; ++p) {
+      const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
+      const double* V = g.vert + 2 * o;
+      bool in = true;
+      for (int i = 0; i < m && in; ++i) {
+        const int j = (i + 1) == m ? 0 : i + 1;
+        const double cr = (V[2 * j] - V[2 * i]) * (y - V[2 * i + 1]) - (V[2 * j + 1] - V[2 * i + 1]) * (x - V[2 * i]);
+        in = cr > 0;
+      }
+      if (in) out = g.lane_len[p];
+    }
+    return out;
+  }
+
+  HTP_HD double heuristic(double x, double y, double yaw) {  // calculate_state_cost :131-158
+    const int G0 = dsc[D_GUIDE0], G1 = dsc[D_GUIDE1];
+    double best = 0.0;
+    int bi = -1;
+    for (int q = G0 + c.lane; q < G1; q += C::width) {
+      const double d = hypot(g.guide[4 * q] - x, g.guide[4 * q + 1] - y);
+      if (bi < 0 || d < best) { best = d; bi = q; }
+    }
+    if (bi < 0) { best = __builtin_huge_val(); bi = 0x7fffffff; }
+    argmin(best, bi);
+    double dtp = best * 100;
+    const double yaw_diff = fabs(angle_wrap(g.guide[4 * bi + 2] - yaw));
+    if (dtp > 2.0) dtp = 100.0;
+    const double dist_to_goal = g.guide[4 * (G1 - 1) + 3] - g.guide[4 * bi + 3];
+    return dtp + yaw_diff * 0.2 + dist_to_goal * 5;
+  }
+
+  HTP_HD static double prio(double cost, double h) {
+    const double b = 50 * h;
+    return b > cost ? b : cost;  // Python max(cost, 50 h)
+  }
+
+  HTP_HD void index(double x, double y, double yaw, int32_t* k) const {
+    k[0] = (int32_t)rint(x / res);
+    k[1] = (int32_t)rint(y / res);
+    k[2] = (int32_t)rint(yaw / yaw_res);
+  }
+
+  // ------------------------------------------------------------ table + heapdict
+  HTP_HD int find(const int32_t* k) const {  // slot of key (existing or empty)
+    uint32_t h = (uint32_t)k[0] * 73856093u ^ (uint32_t)k[1] * 19349663u ^ (uint32_t)k[2] * 83492791u;
+    uint32_t m = (uint32_t)w.cap_slot - 1u;
+    for (uint32_t i = h & m;; i = (i + 1) & m) {
+      const Slot& s = w.slot[i];
+      if (s.state == 0 || (s.kx == k[0] && s.ky == k[1] && s.kt == k[2])) return (int)i;
+    }
+  }
+  HTP_HD void hswap(int i, int j) {
+    const double vi = w.hval[i], vj = w.hval[j];
+    const int32_t si = w.hslot[i], sj = w.hslot[j];
+    w.hval[i] = vj; w.hslot[i] = sj;
+    w.hval[j] = vi; w.hslot[j] = si;
+    w.slot[sj].hpos = i;
+    w.slot[si].hpos = j;
+  }
+  HTP_HD void decrease_key(int i) {
+    while (i) {
+      const int p = (i - 1) >> 1;
+      if (w.hval[p] < w.hval[i]) break;
+      hswap(i, p);
+      i = p;
+    }
+  }
+  HTP_HD void heapify(int i, int n) {
+    for (;;) {
+      const int l = 2 * i + 1, r = 2 * i + 2;
+      int low = (l < n && w.hval[l] < w.hval[i]) ? l : i;
+      if (r < n && w.hval[r] < w.hval[low]) low = r;
+      if (low == i) break;
+      hswap(i, low);
+      i = low;
+    }
+  }
+  HTP_HD int popitem(int& n) {  // -> slot
+    const int s = w.hslot[0];
+    if (n == 1) {
+      n = 0;
+    } else {
+      --n;
+      w.hval[0] = w.hval[n];
+      w.hslot[0] = w.hslot[n];
+      w.slot[w.hslot[0]].hpos = 0;
+      heapify(0, n);
+    }
+    w.slot[s].hpos = -1;
+    return s;
+  }
+  HTP_HD void hset(int s, double v, int& n) {  // heapdict.__setitem__
+    if (w.slot[s].hpos >= 0) {
+      int i = w.slot[s].hpos;
+      while (i) {
+        const int p = (i - 1) >> 1;
+        hswap(i, p);
+        i = p;
+      }
+      popitem(n);
+    }
+    w.hval[n] = v;
+    w.hslot[n] = s;
+    w.slot[s].hpos = n;
+    ++n;
+    decrease_key(n - 1);
+  }
+
+  // ------------------------------------------------------------ motion primitives
+  // Lane m integrates primitive m from pose (x0, y0, yaw0) with n steps into sh.traj.
+  HTP_HD void simulate(int m, double x0, double y0, double yaw0, int n) {
+    const double steer = g.motion[2 * (dsc[D_MOT0] + m)], dir = g.motion[2 * (dsc[D_MOT0] + m) + 1];
+    const double yaw_step = dir * res / wb * tan(steer);
+    const double init_yaw = angle_wrap(yaw0 + yaw_step);
+    const double stop = init_yaw + yaw_step * (double)(n + 1);
+    const int num = n + 2;
+    const double div = (double)(n + 1);
+    const double delta = stop - init_yaw;
+    const double step = delta / div;
+    double ax = 0.0, ay = 0.0;
+    double* T = sh.traj + m * MAXTRAJ * 3;
+    for (int i = 0; i <= n; ++i) {  // numpy linspace (step == 0 branch included), angle_wrap, cumsum
+      const double yi = (step == 0) ? ((double)i / div) * delta + init_yaw : (double)i * step + init_yaw;
+      const double wy = angle_wrap(yi);
+      const double dx = res * cos(wy) * dir;
+      const double dy = res * sin(wy) * dir;
+      ax = (i == 0) ? dx : ax + dx;
+      ay = (i == 0) ? dy : ay + dy;
+      const double ni = (i + 1 == num - 1) ? stop : ((step == 0) ? ((double)(i + 1) / div) * delta + init_yaw
+                                                                : (double)(i + 1) * step + init_yaw);
+      T[3 * i] = x0 + ax;
+      T[3 * i + 1] = y0 + ay;
+      T[3 * i + 2] = angle_wrap(ni);
+    }
+  }
+
+  // simulated_path_cost :306-329 for primitive m (trajectory in sh.traj)
+  HTP_HD double motion_cost(int m, int n, const Node& par) const {
+    const double steer = g.motion[2 * (dsc[D_MOT0] + m)], dir = g.motion[2 * (dsc[D_MOT0] + m) + 1];
+    const double* T = sh.traj + m * MAXTRAJ * 3;
+    double cost = par.cost;
+    double pl = 0.0;
+    for (int i = 0; i < n; ++i) {
+      const double d = hypot(T[3 * (i + 1)] - T[3 * i], T[3 * (i + 1) + 1] - T[3 * i + 1]);
+      pl = (i == 0) ? d : pl + d;
+    }
+    cost += pl;
+    if (dir == -1) cost += 5000;
+    cost += steer * 1;
+    const double sa = atan(par.curv * wb);
+    cost += fabs(steer - sa) * 5;
+    if ((double)par.dir != dir) cost += 1000;
+    return cost;
+  }
+
+  // ------------------------------------------------------------ Reeds-Shepp goal shot
+  // all admissible words from (sx, sy, syaw) to the goal into sh.paths; returns n or -1 (assert/capacity)
+  HTP_HD int rs_paths(double sx, double sy, double syaw) {
+    const double gx = prm[P_GX], gy = prm[P_GY], gyaw = prm[P_GYAW];
+    const double maxc = curv_max;
+    const double dx = gx - sx, dy = gy - sy, dth = gyaw - syaw;
+    const double cc = cos(syaw), ss = sin(syaw);
+    const double x = (cc * dx + ss * dy) * maxc;
+    const double y = (-ss * dx + cc * dy) * maxc;
+    const double xb = x * cos(dth) + y * sin(dth);
+    const double yb = x * sin(dth) - y * cos(dth);
+    const rs::Cand* T = rs::cand_table();
+    for (int k = c.lane; k < 46; k += C::width) {
+      const rs::Cand& cd = T[k];
+      const bool back = cd.arg >= 4;
+      const double bx = back ? xb : x, by = back ? yb : y;
+      const int am = cd.arg & 3;
+      const double ax = (am == 1 || am == 3) ? -bx : bx;
+      const double ay = (am == 2 || am == 3) ? -by : by;
+      const double ap = (am == 1 || am == 2) ? -dth : dth;
+      double t = 0, u = 0, v = 0;
+      int n = 0;
+      if (rs::eval_word(cd.word, ax, ay, ap, t, u, v)) n = rs::lengths_of(cd.lmode, t, u, v, sh.cand_len + 5 * k);
+      sh.cand_n[k] = n;
+    }
+    c.sync();
+    rs::PathSet S{sh.paths, 0, 0};
+    for (int k = 0; k < 46; ++k)
+      if (sh.cand_n[k] > 0) rs::add_path(S, sh.cand_n[k], sh.cand_len + 5 * k, T[k].ty);
+    c.sync();
+    if (S.err) return -1;
+    // generate_local_course must not raise for any path (calc_all_paths samples all of them first)
+    for (int p = 0; p < S.n; ++p)
+      if (!course_ok(sh.paths[p], maxc * res)) return -1;
+    return S.n;
+  }
+
+  // index-only replay of rs::local_course: true unless the reference raises IndexError
+  HTP_HD static bool course_ok(const rs::Path& p, double step) {
+    const int np = rs::point_num(p, step);
+    int ind = 1, cur = 0;
+    double d, pd = (p.len[0] > 0.0) ? step : -step, ll = 0.0;
+    for (int i = 0; i < p.nseg; ++i) {
+      const double l = p.len[i];
+      d = (l > 0.0) ? step : -step;
+      ind -= 1;
+      if (i >= 1 && (p.len[i - 1] * p.len[i]) > 0) pd = -d - ll;
+      else pd = d - ll;
+      while (fabs(pd) <= fabs(l)) {
+        ind += 1;
+        if (ind != cur && ind != cur + 1) return false;
+        cur = ind;
+        if (ind >= np) return false;
+        pd += d;
+      }
+      ll = l - pd - d;
+      ind += 1;
+      if (ind != cur && ind != cur + 1) return false;
+      cur = ind;
+      if (ind >= np) return false;
+    }
+    return true;
+  }
+
+  // Streams the samples of path p (global frame) through the collision test in
+  // chunks of 64; true if any sample collides.
+  HTP_HD bool rs_path_hits(const rs::Path& p, double sx, double sy, double syaw, int64_t& n_pose) {
+    const double maxc = curv_max, step = maxc * res;
+    const double cq = cos(-syaw), sq = sin(-syaw);
+    // segment origins (the previous segment's end sample, zeros first)
+    double ox = 0.0, oy = 0.0, oyaw = 0.0;
+    for (int i = 0; i < p.nseg; ++i) {
+      sh.org[3 * i] = ox; sh.org[3 * i + 1] = oy; sh.org[3 * i + 2] = oyaw;
+      double px, py, pyaw, cs;
+      int dir;
+      rs::interp(p.len[i], p.typ[i], maxc, ox, oy, oyaw, px, py, pyaw, cs, dir);
+      if (p.typ[i] == rs::SEG_S) pyaw = oyaw;
+      ox = px; oy = py; oyaw = pyaw;
+    }
+    c.sync();
+    int base = 0, top = 0;  // chunk [base, base+64), top = highest index written + 1
+    bool hit = false;
+    auto flush = [&](int upto) -> bool {  // test indices [base, upto)
+      c.sync();
+      int h = 0;
+      for (int q = base + c.lane; q < upto; q += C::width) {
+        const int j = q - base;
+        const int si = sh.pseg[j];
+        double lx, ly, lyaw, cs;
+        int dir;
+        if (si < 0) { lx = 0.0; ly = 0.0; lyaw = 0.0; }
+        else {
+          rs::interp(sh.pd[j], p.typ[si], maxc, sh.org[3 * si], sh.org[3 * si + 1], sh.org[3 * si + 2], lx, ly, lyaw,
+                     cs, dir);
+          if (p.typ[si] == rs::SEG_S) lyaw = sh.org[3 * si + 2];
+        }
+        const double gx = cq * lx + sq * ly + sx;
+        const double gy = -sq * lx + cq * ly + sy;
+        const double gyaw = rs::pi2pi(lyaw + syaw);
+        if (pose_hits(gx, gy, gyaw)) h = 1;
+      }
+      n_pose += upto - base;
+      const int r = any(h);
+      c.sync();
+      return r;
+    };
+    auto put = [&](int k, double pdv, int si) -> bool {  // record the final writer of index k
+      if (k >= base + 64) {
+        if (flush(base + 64)) return true;
+        base += 64;
+      }
+      sh.pd[k - base] = pdv;  // uniform: every lane stores the same value
+      sh.pseg[k - base] = si;
+      if (k + 1 > top) top = k + 1;
+      return false;
+    };
+    if (put(0, 0.0, -1)) return true;
+    int ind = 1;
+    double d, pd = (p.len[0] > 0.0) ? step : -step, ll = 0.0;
+    for (int i = 0; i < p.nseg && !hit; ++i) {
+      const double l = p.len[i];
+      d = (l > 0.0) ? step : -step;
+      ind -= 1;
+      if (i >= 1 && (p.len[i - 1] * p.len[i]) > 0) pd = -d - ll;
+      else pd = d - ll;
+      while (fabs(pd) <= fabs(l)) {
+        ind += 1;
+        if (put(ind, pd, i)) { hit = true; break; }
+        pd += d;
+      }
+      if (hit) break;
+      ll = l - pd - d;
+      ind += 1;
+      if (put(ind, l, i)) { hit = true; break; }
+    }
+    if (hit) return true;
+    return flush(top);
+  }
+
+  // RS goal shot: index of the path taken (generation order) or -1; cost in *out_cost
+  HTP_HD int goal_shot(const Node& cur, double& out_cost, int& err, int64_t& n_pose, int64_t& n_checks) {
+    const int np = rs_paths(cur.x, cur.y, cur.yaw);
+    if (np < 0) { err = 1; return -1; }
+    if (np == 0) return -1;
+    // calculate_reeds_shepp_path_cost :129-160 + heapdict insertion in path order
+    int hn = 0;
+    for (int k = 0; k < np; ++k) {
+      const rs::Path& P = sh.paths[k];
+      double cost = cur.cost;
+      int nneg = 0;
+      for (int j = 0; j < P.nseg; ++j) nneg += P.len[j] < 0 ? 1 : 0;
+      cost += (double)(5000 * nneg + (P.nseg - nneg));
+      cost += 1000.0;
+      cost += maxsteer * 1 * 1;
+      double ds = 0.0;
+      for (int j = 0; j + 1 < P.nseg; ++j) {
+        const double a = P.typ[j] == rs::SEG_R ? -maxsteer : 0.0;
+        const double b = P.typ[j + 1] == rs::SEG_R ? -maxsteer : 0.0;
+        ds = ds + fabs(b - a);
+      }
+      cost += ds;
+      // heapdict __setitem__ of a new key
+      int i = hn++;
+      sh.rval[i] = cost;
+      sh.rkey[i] = k;
+      while (i) {
+        const int pp = (i - 1) >> 1;
+        if (sh.rval[pp] < sh.rval[i]) break;
+        const double tv = sh.rval[pp]; sh.rval[pp] = sh.rval[i]; sh.rval[i] = tv;
+        const int tk = sh.rkey[pp]; sh.rkey[pp] = sh.rkey[i]; sh.rkey[i] = tk;
+        i = pp;
+      }
+    }
+    while (hn > 0) {
+      const int k = sh.rkey[0];
+      const double v = sh.rval[0];
+      if (hn == 1) hn = 0;
+      else {
+        --hn;
+        sh.rval[0] = sh.rval[hn];
+        sh.rkey[0] = sh.rkey[hn];
+        int i = 0;
+        for (;;) {
+          const int l = 2 * i + 1, r = 2 * i + 2;
+          int low = (l < hn && sh.rval[l] < sh.rval[i]) ? l : i;
+          if (r < hn && sh.rval[r] < sh.rval[low]) low = r;
+          if (low == i) break;
+          const double tv = sh.rval[low]; sh.rval[low] = sh.rval[i]; sh.rval[i] = tv;
+          const int tk = sh.rkey[low]; sh.rkey[low] = sh.rkey[i]; sh.rkey[i] = tk;
+          i = low;
+        }
+      }
+      const rs::Path& P = sh.paths[k];
+      if (!(P.L / curv_max < 1000.0)) continue;  // path.L < MIN_LENGTH_TO_GOAL (checked first: same outcome)
+      ++n_checks;
+      if (!rs_path_hits(P, cur.x, cur.y, cur.yaw, n_pose)) {
+        out_cost = v;
+        return k;
+      }
+    }
+    return -1;
+  }
+
+  HTP_HD bool traj_hits_single(double x, double y, double yaw, int64_t& n_pose) {
+    int h = 0;
+    if (c.lane == 0) h = pose_hits(x, y, yaw) ? 1 : 0;
+    ++n_pose;
+    return any(h);
+  }
+
+  // ------------------------------------------------------------ search
+  HTP_HD int new_node(int& nn) {
+    if (nn >= w.cap_node) return -1;
+    return nn++;
+  }
+
+  HTP_HD void run(Out& o, int32_t* log, int cap_log) {
+    o = Out{};
+    const int max_nodes = (int)prm[P_MAXNODES];
+    for (int q = c.lane; q < w.cap_slot; q += C::width) {
+      w.slot[q].state = 0;
+      w.slot[q].hpos = -1;
+    }
+    c.sync();
+    int32_t sk[3], gk[3];
+    index(prm[P_SX], prm[P_SY], prm[P_SYAW], sk);
+    index(prm[P_GX], prm[P_GY], prm[P_GYAW], gk);
+    int nn = 0, hn = 0;
+    // start node
+    Node st{};
+    st.x = prm[P_SX]; st.y = prm[P_SY]; st.yaw = prm[P_SYAW]; st.cost = 0.0; st.curv = 0.0;
+    st.kx = sk[0]; st.ky = sk[1]; st.kt = sk[2];
+    st.pkx = sk[0]; st.pky = sk[1]; st.pkt = sk[2];
+    st.parent = -1; st.kind = 0; st.aux = 0; st.dir = 1;
+    const double h0 = heuristic(st.x, st.y, st.yaw);
+    if (traj_hits_single(st.x, st.y, st.yaw, o.n_pose) || traj_hits_single(prm[P_GX], prm[P_GY], prm[P_GYAW], o.n_pose)) {
+      o.n_checks += 2;
+      o.status = ST_START_GOAL_BLOCKED;
+      return;
+    }
+    o.n_checks += 2;
+    {
+      const int id = new_node(nn);
+      if (c.lane == 0 || C::width == 1) w.node[id] = st;
+      const int s = find(sk);
+      if (c.lane == 0 || C::width == 1) {
+        w.slot[s].kx = sk[0]; w.slot[s].ky = sk[1]; w.slot[s].kt = sk[2];
+        w.slot[s].state = 1; w.slot[s].node = id;
+      }
+      c.sync();
+      hset(s, prio(0.0, h0), hn);
+      c.sync();
+    }
+    int counter = 0, status = ST_NO_PATH, goal_node = -1;
+    for (;;) {
+      if (counter > max_nodes) { status = ST_MAX_NODES; break; }
+      counter += 1;
+      if (hn == 0) { status = ST_NO_PATH; break; }
+      const int s = popitem(hn);
+      c.sync();
+      const int cid = w.slot[s].node;
+      if (c.lane == 0 || C::width == 1) w.slot[s].state = 2;
+      const Node cur = w.node[cid];
+      if (o.n_expanded < cap_log && (c.lane == 0 || C::width == 1)) {
+        log[3 * o.n_expanded] = cur.kx; log[3 * o.n_expanded + 1] = cur.ky; log[3 * o.n_expanded + 2] = cur.kt;
+      }
+      o.n_expanded += 1;
+      c.sync();
+      // goal extension
+      int err = 0;
+      double gcost = 0.0;
+      const int pk = goal_shot(cur, gcost, err, o.n_pose, o.n_checks);
+      if (err) { status = ST_RS_ERROR; break; }
+      int gid = -1;
+      if (pk >= 0) {
+        gid = new_node(nn);
+        if (gid < 0) { status = ST_CAPACITY; break; }
+        Node gn{};
+        gn.x = prm[P_GX]; gn.y = prm[P_GY]; gn.yaw = prm[P_GYAW];  // end pose (unused: never expanded)
+        gn.cost = gcost; gn.curv = 0.0; gn.kx = gk[0]; gn.ky = gk[1]; gn.kt = gk[2];
+        gn.pkx = cur.kx; gn.pky = cur.ky; gn.pkt = cur.kt; gn.parent = cid; gn.kind = 2; gn.aux = (int16_t)pk;
+        gn.dir = 1;
+        if (c.lane == 0 || C::width == 1) w.node[gid] = gn;
+      }
+      // check_the_arrival :464-495 (goal pose = goal_node.traj[0])
+      if (fabs(cur.x - prm[P_GX]) < res && fabs(cur.y - prm[P_GY]) < res &&
+          fabs(angle_wrap(cur.yaw - prm[P_GYAW])) < yaw_res) {
+        gid = new_node(nn);
+        if (gid < 0) { status = ST_CAPACITY; break; }
+        Node gn = cur;
+        gn.kx = gk[0]; gn.ky = gk[1]; gn.kt = gk[2];
+        if (c.lane == 0 || C::width == 1) {
+          w.node[gid] = gn;
+          w.node[cid].kx = gk[0]; w.node[cid].ky = gk[1]; w.node[cid].kt = gk[2];
+        }
+      }
+      c.sync();
+      if (gid >= 0) {
+        const int gs = find(gk);
+        if (c.lane == 0 || C::width == 1) {
+          w.slot[gs].kx = gk[0]; w.slot[gs].ky = gk[1]; w.slot[gs].kt = gk[2];
+          w.slot[gs].state = 2; w.slot[gs].node = gid;
+        }
+        c.sync();
+        goal_node = gid;
+        status = ST_FOUND;
+        break;
+      }
+      // expansion: all primitives share the parent's search length
+      const double L = search_length(cur.x, cur.y);
+      const int n = (int)rint(L / res);
+      if (n < 1 || n + 1 > MAXTRAJ) { status = ST_BAD_INPUT; break; }
+      for (int m = c.lane; m < nmot; m += C::width) {
+        simulate(m, cur.x, cur.y, cur.yaw, n);
+        sh.hit[m] = 0;
+      }
+      c.sync();
+      const int tot = nmot * (n + 1);
+      for (int q = c.lane; q < tot; q += C::width) {
+        const int m = q / (n + 1), i = q - m * (n + 1);
+        const double* T = sh.traj + (m * MAXTRAJ + i) * 3;
+        if (pose_hits(T[0], T[1], T[2])) sh.hit[m] = 1;
+      }
+      o.n_pose += tot;
+      o.n_checks += nmot;
+      c.sync();
+      for (int m = c.lane; m < nmot; m += C::width) {
+        sh.ccost[m] = motion_cost(m, n, cur);
+        const double steer = g.motion[2 * (dsc[D_MOT0] + m)];
+        sh.ccurv[m] = tan(steer) / wb;
+        const double* T = sh.traj + (m * MAXTRAJ + n) * 3;
+        index(T[0], T[1], T[2], sh.ckey + 3 * m);
+      }
+      c.sync();
+      bool cap = false;
+      for (int m = 0; m < nmot; ++m) {
+        if (sh.hit[m]) continue;
+        const int32_t* k = sh.ckey + 3 * m;
+        const int s2 = find(k);
+        const int state = w.slot[s2].state;
+        if (state == 2) continue;
+        const double cost = sh.ccost[m];
+        if (state == 1 && !(cost < w.node[w.slot[s2].node].cost)) continue;
+        const int id = new_node(nn);
+        if (id < 0) { cap = true; break; }
+        const double* T = sh.traj + (m * MAXTRAJ + n) * 3;
+        Node ch{};
+        ch.x = T[0]; ch.y = T[1]; ch.yaw = T[2]; ch.cost = cost; ch.curv = sh.ccurv[m];
+        ch.kx = k[0]; ch.ky = k[1]; ch.kt = k[2];
+        ch.pkx = cur.kx; ch.pky = cur.ky; ch.pkt = cur.kt;
+        ch.parent = cid; ch.kind = 1; ch.aux = (int16_t)m;
+        ch.dir = (int32_t)g.motion[2 * (dsc[D_MOT0] + m) + 1];
+        const double h = heuristic(ch.x, ch.y, ch.yaw);
+        if (c.lane == 0 || C::width == 1) {
+          w.node[id] = ch;
+          w.slot[s2].kx = k[0]; w.slot[s2].ky = k[1]; w.slot[s2].kt = k[2];
+          w.slot[s2].state = 1; w.slot[s2].node = id;
+        }
+        c.sync();
+        hset(s2, prio(cost, h), hn);
+        c.sync();
+      }
+      if (cap) { status = ST_CAPACITY; break; }
+    }
+    o.counter = counter;
+    o.status = status;
+    (void)goal_node;
+  }
+
+  // get_path_from_expanded_nodes :429-454 -> number of samples written (or needed)
+  HTP_HD int backtrack(int32_t* chain, int cap_chain, double* px, double* py, double* pyaw, double* pdir,
+                       double* pk, int cap_path, int& status) {
+    // the start node is node 0; its grid index is the goal's if the start itself
+    // arrived (check_the_arrival relabels the node object, :492-493)
+    const int32_t sk[3] = {w.node[0].kx, w.node[0].ky, w.node[0].kt};
+    int32_t gk[3];
+    index(prm[P_GX], prm[P_GY], prm[P_GYAW], gk);
+    int32_t k[3] = {gk[0], gk[1], gk[2]};
+    int s = find(k);
+    if (w.slot[s].state != 2) return 0;
+    int nc = 0;
+    while (!(k[0] == sk[0] && k[1] == sk[1] && k[2] == sk[2])) {
+      if (nc >= cap_chain) { status = ST_BACKTRACK; return 0; }
+      const int id = w.slot[s].node;
+      if (c.lane == 0 || C::width == 1) chain[nc] = id;
+      ++nc;
+      const Node& nd = w.node[id];
+      k[0] = nd.pkx; k[1] = nd.pky; k[2] = nd.pkt;
+      s = find(k);
+      if (w.slot[s].state != 2) { status = ST_BACKTRACK; return 0; }  // the reference raises KeyError
+    }
+    c.sync();
+    int off = 0;
+    for (int ci = nc - 1; ci >= 0; --ci) {
+      const Node nd = w.node[chain[ci]];
+      if (nd.kind == 0) {
+        if (off < cap_path && (c.lane == 0 || C::width == 1)) {
+          px[off] = nd.x; py[off] = nd.y; pyaw[off] = nd.yaw; pdir[off] = 1.0; pk[off] = 0.0;
+        }
+        off += 1;
+      } else if (nd.kind == 1) {
+        const Node par = w.node[nd.parent];
+        const double L = search_length(par.x, par.y);
+        const int n = (int)rint(L / res);
+        if (c.lane == 0 || C::width == 1) simulate(nd.aux, par.x, par.y, par.yaw, n);
+        c.sync();
+        const double dir = g.motion[2 * (dsc[D_MOT0] + nd.aux) + 1];
+        const double kv = tan(g.motion[2 * (dsc[D_MOT0] + nd.aux)]) / wb;
+        const double* T = sh.traj + nd.aux * MAXTRAJ * 3;
+        for (int i = c.lane; i <= n; i += C::width)
+          if (off + i < cap_path) {
+            px[off + i] = T[3 * i]; py[off + i] = T[3 * i + 1]; pyaw[off + i] = T[3 * i + 2];
+            pdir[off + i] = dir; pk[off + i] = kv;
+          }
+        off += n + 1;
+        c.sync();
+      } else {
+        const Node par = w.node[nd.parent];
+        (void)rs_paths(par.x, par.y, par.yaw);
+        const rs::Path P = sh.paths[nd.aux];
+        c.sync();
+        rs::NullSink ns;
+        const int cnt = rs::local_course(P, curv_max, curv_max * res, ns);
+        if (cnt > 0 && off + cnt <= cap_path && (c.lane == 0 || C::width == 1)) {
+          struct DSink {
+            double *x, *y, *yaw, *cs, *dir;
+            int limit;
+            double sx, sy, syaw, cq, sq;
+            HTP_HD void put(int kk, double lx, double ly, double lyaw, double cc, int d) const {
+              if (kk >= limit) return;
+              x[kk] = cq * lx + sq * ly + sx;
+              y[kk] = -sq * lx + cq * ly + sy;
+              yaw[kk] = rs::pi2pi(lyaw + syaw);
+              cs[kk] = cc;
+              dir[kk] = (double)d;
+            }
+          } gs{px + off, py + off, pyaw + off, pk + off, pdir + off, cnt, par.x, par.y, par.yaw, cos(-par.yaw),
+               sin(-par.yaw)};
+          rs::local_course(P, curv_max, curv_max * res, gs);
+        }
+        off += cnt > 0 ? cnt : 0;
+        c.sync();
+      }
+    }
+    return off;
+  }
+};
+
+}  // namespace ha
+}  // namespace htp

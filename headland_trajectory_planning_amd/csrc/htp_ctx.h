@@ -23,6 +23,10 @@ struct htp_ctx {
   void* rs_scratch = nullptr;
   size_t rs_scratch_bytes = 0;
   hipEvent_t rs_ev0 = nullptr, rs_ev1 = nullptr;
+  // Hybrid A* batch (htp_hastar.hip)
+  void* ha_ws = nullptr;
+  size_t ha_ws_bytes = 0;
+  hipEvent_t ha_ev0 = nullptr, ha_ev1 = nullptr;
 };
 
 static inline int fail(htp_ctx* c, const std::string& m) {

@@ -91,6 +91,8 @@ htp_ctx* htp_create(int32_t device) {
   (void)hipEventCreate(&c->ev1);
   (void)hipEventCreate(&c->rs_ev0);
   (void)hipEventCreate(&c->rs_ev1);
+  (void)hipEventCreate(&c->ha_ev0);
+  (void)hipEventCreate(&c->ha_ev1);
   return c;
 }
 
@@ -104,6 +106,9 @@ void htp_destroy(htp_ctx* c) {
   if (c->rs_scratch) (void)hipFree(c->rs_scratch);
   if (c->rs_ev0) (void)hipEventDestroy(c->rs_ev0);
   if (c->rs_ev1) (void)hipEventDestroy(c->rs_ev1);
+  if (c->ha_ws) (void)hipFree(c->ha_ws);
+  if (c->ha_ev0) (void)hipEventDestroy(c->ha_ev0);
+  if (c->ha_ev1) (void)hipEventDestroy(c->ha_ev1);
   delete c;
 }
 

@@ -21,7 +21,8 @@ def build():
     if os.path.exists(SO) and os.path.getmtime(SO) >= max(os.path.getmtime(s) for s in srcs):
         return SO
     subprocess.check_call(["g++", "-O2", "-fno-builtin", "-std=c++17", "-shared", "-fPIC", "-o", SO,
-                           os.path.join(CSRC, "htp_hostsim.cpp"), os.path.join(CSRC, "rs_hostsim.cpp")])
+                           os.path.join(CSRC, "htp_hostsim.cpp"), os.path.join(CSRC, "rs_hostsim.cpp"),
+                           os.path.join(CSRC, "hastar_hostsim.cpp")])
     return SO
 
 
@@ -106,4 +107,26 @@ def rs_host(queries):
     out["path_offsets"] = np.concatenate([[0], np.cumsum(npaths)]).astype(np.int64)
     out["point_offsets"] = np.concatenate([[0], np.cumsum(npts_path)]).astype(np.int64)
     out["n_paths"], out["n_points"] = int(out["path_offsets"][-1]), int(out["point_offsets"][-1])
+    return out
+
+
+def hastar_host(problems, cap_path=4096):
+    """Host build of csrc/hastar_core.h (serial lane), same result object as
+    Context.hastar.  TEST-ONLY."""
+    l = lib()
+    f = l.htp_hostsim_hastar
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.POINTER(_native.HaBatch), ctypes.POINTER(_native.HaResult)]
+    pk = _native.HastarPacked(problems, cap_path=cap_path)
+    res = _native.HastarResults(pk)
+    assert f(ctypes.byref(pk.struct()), ctypes.byref(res.struct())) == 0
+    return res
+
+
+def as_dicts(res):
+    out = []
+    for b in range(len(res.status)):
+        xs, ys, yaws, dirs, ks = res.path(b)
+        out.append(dict(xs=xs, ys=ys, yaws=yaws, dirs=dirs, ks=ks, counter=int(res.counter[b]),
+                        status=int(res.status[b]), expanded=res.expansions(b), n_pose=int(res.n_pose[b])))
     return out

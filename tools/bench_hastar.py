@@ -1,0 +1,86 @@
+"""Hybrid A* batch throughput: B seeded headland
+searches (King / Reeds-Shepp shots, plan_resolution 0.2, max_nodes 400 as
+R/path_planner/headland_path_planning.py:219) in one launch on one GPU, inputs
+resident in HBM, timed with hipEvents on the launch stream
+(htp_hastar_last_ms).  CPU baseline: the serial host build of the same core
+(test infrastructure) on a bounded sample.  Prints one JSON line:
+searches/s, footprint pose-tests/s, expansions/s."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--max-nodes", type=int, default=400)
+    ap.add_argument("--cpu-sample", type=int, default=64)
+    args = ap.parse_args()
+    import torch
+
+    import _ha_util as U
+    import _hostsim as H
+    from headland_trajectory_planning_amd import _native
+    dev = torch.device("cuda", 0)
+    t0 = time.perf_counter()
+    uniq = [U.scenario(s, max_nodes=args.max_nodes) for s in range(min(args.batch, 512))]
+    probs = [uniq[i % len(uniq)] for i in range(args.batch)]
+    gen_s = time.perf_counter() - t0
+    ctx = _native.Context(0)
+    pk = _native.HastarPacked(probs, cap_path=4096, cap_log=0)
+    B = pk.batch
+    dv = {n: torch.from_numpy(np.ascontiguousarray(getattr(pk, n))).to(dev)
+          for n in ("params", "desc", "poly_off", "vertices", "lane_len", "guide", "motions")}
+    out = {"status": torch.empty(B, dtype=torch.int32, device=dev),
+           "counter": torch.empty(B, dtype=torch.int32, device=dev),
+           "n_path": torch.empty(B, dtype=torch.int32, device=dev),
+           "n_expanded": torch.empty(B, dtype=torch.int32, device=dev),
+           "n_pose": torch.empty(B, dtype=torch.int64, device=dev)}
+    for k in ("x", "y", "yaw", "dir", "k"):
+        out[k] = torch.empty((B, pk.cap_path), dtype=torch.float64, device=dev)
+    ptrs = {k: v.data_ptr() for k, v in dv.items()}
+    optrs = {k: v.data_ptr() for k, v in out.items()}
+    optrs["expanded"] = None
+    stream = torch.cuda.current_stream().cuda_stream
+    for _ in range(args.warmup):
+        ctx.hastar_device(pk, ptrs, optrs, stream)
+    torch.cuda.synchronize()
+    ms = []
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.hastar_device(pk, ptrs, optrs, stream)
+        ms.append(ctx.hastar_last_ms())
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t) / args.steps
+    st = out["status"].cpu().numpy()
+    ne = int(out["n_expanded"].sum().item())
+    npose = int(out["n_pose"].sum().item())
+    kms = float(np.mean(ms))
+    # CPU baseline: serial host build of the same core on the first problems
+    n = min(args.cpu_sample, B)
+    t = time.perf_counter()
+    hres = H.hastar_host(probs[:n])
+    cpu_s = time.perf_counter() - t
+    line = {"metric": "hybrid A* headland searches/s (King, res 0.2, max_nodes %d)" % args.max_nodes,
+            "value": B / (kms / 1e3), "unit": "searches/s", "batch": B, "kernel_ms": kms, "wall_ms": wall * 1e3,
+            "pose_tests_per_s": npose / (kms / 1e3), "expansions_per_s": ne / (kms / 1e3),
+            "mean_expansions": ne / B, "status_hist": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
+            "gen_s": gen_s,
+            "cpu_baseline": {"value": n / cpu_s, "unit": "searches/s", "cores": 1, "kind": "port",
+                             "sample": f"first {n} searches, serial host build of csrc/hastar_core.h (g++ -O2)",
+                             "pose_tests_per_s": float(hres.n_pose.sum()) / cpu_s}}
+    print(json.dumps(line))
+
+
+if __name__ == "__main__":
+    main()
