@@ -72,20 +72,34 @@ struct LocalBlock {
 
   HTP_HD HTP_FI static int pk(int r, int c) { return r * (r + 1) / 2 + c; }
 
-  HTP_HD HTP_FI void factor() {  // unpivoted LDL^T of K (inertia = signs of D)
+  bool piv;            // Bunch-Kaufman would interchange: use the pivoted path
+
+  // Unpivoted LDL^T of K (inertia = signs of D), in place.  With H_zz
+  // positive definite (every multiplier pivot > 0) this is a Cholesky of H_zz
+  // followed by one of the negative definite 2x2 Schur complement: stable.
+  // The reduced Hessian may however be indefinite on the multiplier block
+  // itself (only its restriction to null(C_z) must be positive); a
+  // non-positive multiplier pivot sets `piv` and the block is redone by
+  // ObcaSolver::local_pivoted (Bunch-Kaufman with interchanges, exact
+  // inertia, stable solves).  The common case keeps this small,
+  // register-resident code.
+  HTP_HD HTP_FI void factor() {
     neg = 0;
     zero = 0;
+    piv = false;
     for (int k = 0; k < NL; ++k) {
       double dk = K[pk(k, k)];
       for (int j = 0; j < k; ++j) dk -= K[pk(k, j)] * K[pk(k, j)] * K[pk(j, j)];
-      if (dk == 0.0) { zero = 1; dk = 1.0; }
-      if (dk < 0.0) ++neg;
-      K[pk(k, k)] = dk;
       for (int r = k + 1; r < NL; ++r) {
         double v = K[pk(r, k)];
         for (int j = 0; j < k; ++j) v -= K[pk(r, j)] * K[pk(k, j)] * K[pk(j, j)];
-        K[pk(r, k)] = v / dk;
+        K[pk(r, k)] = v;
       }
+      if (k < NZ && !(dk > 0.0)) piv = true;
+      if (dk == 0.0) { zero = 1; dk = 1.0; }
+      if (dk < 0.0) ++neg;
+      K[pk(k, k)] = dk;
+      for (int r = k + 1; r < NL; ++r) K[pk(r, k)] = K[pk(r, k)] / dk;
     }
   }
   HTP_HD HTP_FI void solve(double* v) const {  // in place K^-1 v
@@ -96,6 +110,110 @@ struct LocalBlock {
       for (int r = k + 1; r < NL; ++r) v[k] -= K[pk(r, k)] * v[r];
   }
 };
+
+// Bunch-Kaufman LDL^T (LAPACK dsytf2 / dsytrs, lower) of a packed symmetric
+// n x n matrix, for the rare local blocks that need interchanges.  Run-time
+// indexing: these live in their own (not inlined) frame.
+HTP_HD inline double& pk_at(double* K, int r, int c) { return r >= c ? K[r * (r + 1) / 2 + c] : K[c * (c + 1) / 2 + r]; }
+HTP_HD inline double pk_at(const double* K, int r, int c) { return r >= c ? K[r * (r + 1) / 2 + c] : K[c * (c + 1) / 2 + r]; }
+
+HTP_HD inline void bk_factor_packed(double* K, int* ip, int n, int& neg, int& zero) {
+  const double alpha = 0.6403882032022076;
+  neg = 0;
+  zero = 0;
+  int k = 0;
+  while (k < n) {
+    int kstep = 1, kp = k;
+    const double absakk = fabs(pk_at(K, k, k));
+    int imax = k;
+    double colmax = 0.0;
+    for (int r = k + 1; r < n; ++r)
+      if (fabs(pk_at(K, r, k)) > colmax) { colmax = fabs(pk_at(K, r, k)); imax = r; }
+    if (!(absakk >= alpha * colmax) && !(absakk == 0.0 && colmax == 0.0)) {
+      double rowmax = 0.0;
+      for (int j = k; j < n; ++j)
+        if (j != imax && fabs(pk_at(K, imax, j)) > rowmax) rowmax = fabs(pk_at(K, imax, j));
+      if (absakk >= alpha * colmax * (colmax / rowmax)) kp = k;
+      else if (fabs(pk_at(K, imax, imax)) >= alpha * rowmax) kp = imax;
+      else { kp = imax; kstep = 2; }
+    }
+    const int kk = k + kstep - 1;
+    if (kp != kk) {
+      for (int j = k; j < n; ++j)
+        if (j != kk && j != kp) { const double t = pk_at(K, kk, j); pk_at(K, kk, j) = pk_at(K, kp, j); pk_at(K, kp, j) = t; }
+      const double t = pk_at(K, kk, kk); pk_at(K, kk, kk) = pk_at(K, kp, kp); pk_at(K, kp, kp) = t;
+    }
+    if (kstep == 1) {
+      double d = pk_at(K, k, k);
+      if (d == 0.0) { zero = 1; d = 1.0; pk_at(K, k, k) = 1.0; }
+      if (d < 0.0) ++neg;
+      const double id = 1.0 / d;
+      for (int r = k + 1; r < n; ++r) {
+        const double lr = pk_at(K, r, k) * id;
+        for (int q = k + 1; q <= r; ++q) pk_at(K, r, q) -= lr * pk_at(K, q, k);
+      }
+      for (int r = k + 1; r < n; ++r) pk_at(K, r, k) *= id;
+      ip[k] = kp;
+    } else {
+      const double d11 = pk_at(K, k, k), d21 = pk_at(K, k + 1, k), d22 = pk_at(K, k + 1, k + 1);
+      const double det = d11 * d22 - d21 * d21;
+      if (det < 0.0) neg += 1;
+      else if (det > 0.0) neg += (d11 + d22 < 0.0) ? 2 : 0;
+      else zero = 1;
+      const double i11 = d22 / det, i22 = d11 / det, i21 = -d21 / det;
+      for (int r = n - 1; r >= k + 2; --r) {  // descending: rows q < r still hold their original columns
+        const double a1 = pk_at(K, r, k), a2 = pk_at(K, r, k + 1);
+        const double l1 = a1 * i11 + a2 * i21, l2 = a1 * i21 + a2 * i22;
+        for (int q = k + 2; q <= r; ++q) pk_at(K, r, q) -= l1 * pk_at(K, q, k) + l2 * pk_at(K, q, k + 1);
+        pk_at(K, r, k) = l1;
+        pk_at(K, r, k + 1) = l2;
+      }
+      ip[k] = -(kp + 1);
+      ip[k + 1] = -(kp + 1);
+    }
+    k += kstep;
+  }
+}
+
+HTP_HD inline void bk_solve_packed(const double* K, const int* ip, int n, double* v) {
+  int k = 0;
+  while (k < n) {
+    if (ip[k] >= 0) {
+      const int kp = ip[k];
+      if (kp != k) { const double t = v[k]; v[k] = v[kp]; v[kp] = t; }
+      for (int r = k + 1; r < n; ++r) v[r] -= pk_at(K, r, k) * v[k];
+      v[k] /= pk_at(K, k, k);
+      k += 1;
+    } else {
+      const int kp = -ip[k] - 1;
+      if (kp != k + 1) { const double t = v[k + 1]; v[k + 1] = v[kp]; v[kp] = t; }
+      for (int r = k + 2; r < n; ++r) v[r] -= pk_at(K, r, k) * v[k] + pk_at(K, r, k + 1) * v[k + 1];
+      const double d11 = pk_at(K, k, k), d21 = pk_at(K, k + 1, k), d22 = pk_at(K, k + 1, k + 1);
+      const double det = d11 * d22 - d21 * d21;
+      const double b1 = v[k], b2 = v[k + 1];
+      v[k] = (d22 * b1 - d21 * b2) / det;
+      v[k + 1] = (-d21 * b1 + d11 * b2) / det;
+      k += 2;
+    }
+  }
+  k = n - 1;
+  while (k >= 0) {
+    if (ip[k] >= 0) {
+      for (int r = k + 1; r < n; ++r) v[k] -= pk_at(K, r, k) * v[r];
+      const int kp = ip[k];
+      if (kp != k) { const double t = v[k]; v[k] = v[kp]; v[kp] = t; }
+      k -= 1;
+    } else {
+      for (int r = k + 1; r < n; ++r) {
+        v[k] -= pk_at(K, r, k) * v[r];
+        v[k - 1] -= pk_at(K, r, k - 1) * v[r];
+      }
+      const int kp = -ip[k] - 1;
+      if (kp != k) { const double t = v[k]; v[k] = v[kp]; v[kp] = t; }
+      k -= 2;
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------
 template <class Ctx, int EN_ = 4, int EM_ = 4>
@@ -679,6 +797,19 @@ struct ObcaSolver {
     (void)NL;
   }
 
+  // Local block p with Bunch-Kaufman interchanges (rare): rebuild, factor,
+  // solve the nrhs right-hand sides V[k*NL ...] in place.
+  template <int EN, int EM>
+  __attribute__((noinline)) HTP_HD void local_pivoted(int p, bool ls, double dw, double dc, double* V, int nrhs,
+                                                      int* inertia) const {
+    constexpr int NL = LocalBlock<EN, EM>::NL;
+    LocalBlock<EN, EM> B;
+    build_local<EN, EM>(B, p, ls, dw, dc);
+    int ip[NL];
+    bk_factor_packed(B.K, ip, NL, inertia[0], inertia[1]);
+    for (int k = 0; k < nrhs; ++k) bk_solve_packed(B.K, ip, NL, V + k * NL);
+  }
+
   template <int EN, int EM>
   HTP_HD HTP_FI void local_factor_sweep(bool ls, double dw, double dc, int& neg, int& zero) {
     gd* PS = A(L.pairS);
@@ -686,14 +817,25 @@ struct ObcaSolver {
       LocalBlock<EN, EM> B;
       build_local<EN, EM>(B, p, ls, dw, dc);
       B.factor();
-      neg += B.neg;
-      zero |= B.zero;
       constexpr int NL = LocalBlock<EN, EM>::NL;
+      double Vp[3 * NL];
+      int bneg = B.neg, bzero = B.zero;
+      if (B.piv) {
+        for (int col = 0; col < 3; ++col)
+          for (int r = 0; r < NL; ++r) Vp[col * NL + r] = B.B[r][col];
+        int pn[2];
+        local_pivoted<EN, EM>(p, ls, dw, dc, Vp, 3, pn);
+        bneg = pn[0];
+        bzero = pn[1];
+      }
+      neg += bneg;
+      zero |= bzero;
       double S[6] = {0, 0, 0, 0, 0, 0};
       for (int col = 0; col < 3; ++col) {
         double v[NL];
         for (int r = 0; r < NL; ++r) v[r] = B.B[r][col];
-        B.solve(v);
+        if (B.piv) for (int r = 0; r < NL; ++r) v[r] = Vp[col * NL + r];
+        else B.solve(v);
         // S(:,col) = B' v
         for (int row = 0; row <= col; ++row) {
           double acc = 0.0;
@@ -729,7 +871,15 @@ struct ObcaSolver {
       const int re = D.ePair + 2 * p;
       v[NZ] = bc[re];
       v[NZ + 1] = bc[re + 1];
-      B.solve(v);
+      if (B.piv) {
+        double vp[NL];
+        int pn[2];
+        for (int r = 0; r < NL; ++r) vp[r] = v[r];
+        local_pivoted<EN, EM>(p, ls, dw, dc, vp, 1, pn);
+        for (int r = 0; r < NL; ++r) v[r] = vp[r];
+      } else {
+        B.solve(v);
+      }
       for (int col = 0; col < 3; ++col) {
         double acc = 0.0;
         for (int r = 0; r < NL; ++r) acc += B.B[r][col] * v[r];
@@ -761,7 +911,15 @@ struct ObcaSolver {
       v[NZ] = bc[re];
       v[NZ + 1] = bc[re + 1];
       for (int r = 0; r < NL; ++r) v[r] -= B.B[r][0] * dpx + B.B[r][1] * dpy + B.B[r][2] * dth;
-      B.solve(v);
+      if (B.piv) {
+        double vp[NL];
+        int pn[2];
+        for (int r = 0; r < NL; ++r) vp[r] = v[r];
+        local_pivoted<EN, EM>(p, ls, dw, dc, vp, 1, pn);
+        for (int r = 0; r < NL; ++r) v[r] = vp[r];
+      } else {
+        B.solve(v);
+      }
       for (int j = 0; j < en; ++j) ox[mu0 + j] = v[j];
       for (int j = 0; j < em; ++j) ox[la0 + j] = v[EN + j];
       oc[re] = v[NZ];
@@ -1473,6 +1631,24 @@ struct ObcaSolver {
     c.sync();
     long long t1 = c.clock();
     cyc[0] += t1 - t0;
+    // Inertia bookkeeping.  Each eliminated block is a saddle-point matrix
+    // [H, C'; C, -dc I] whose constraint rows C have full row rank, so it has
+    // at least as many negative eigenvalues as rows (Sylvester on the Schur
+    // complement).  Every local block therefore contributes >= 2 negatives
+    // and the stage system >= 5N: the total equals IPOPT's required count iff
+    // the local blocks hold exactly 2P and the stage system exactly 5N.
+    // Extra local negatives => wrong inertia, decided without the stage
+    // factorization.  With exact dynamics (dc == 0) the stage count is 5N iff
+    // every Riccati pivot Rt is positive definite; dc > 0 takes the block
+    // Bunch-Kaufman path below.
+    // (A zero local pivot only needs reporting: IPOPT's reaction -- dc, then
+    // dw -- does not depend on the stage system.)
+    if (zero > 0 || neg != 2 * D.P) {
+      use_ric = false;
+      neg_out = -1;
+      zero_out = zero;
+      return;
+    }
     for (int i = c.lane; i < N; i += c.width) assemble_stage(i, ls, dw, dc);
     c.sync();
     long long t2 = c.clock();
@@ -1481,7 +1657,7 @@ struct ObcaSolver {
       const int bad = riccati_factor();
       use_ric = true;
       cyc[2] += c.clock() - t2;
-      neg_out = neg + (bad ? -1 : NS * N) + NS + D.md;
+      neg_out = bad ? -1 : neg + NS * N + NS + D.md;
       zero_out = zero;
       return;
     }
@@ -2084,6 +2260,7 @@ struct ObcaSolver {
           accepted = true; a_primal = alpha; a_test = alpha; th_acc = th_t;
           break;
         }
+        HTP_TRACE("[trace]   ls alpha=%.17g th_t=%.17g ph_t=%.17g (theta=%.17g phi=%.17g gBD=%.17g amax=%.17g)\n", alpha, th_t, ph_t, theta, phi, gBD, alpha_max);
         if (first && th_t >= theta && o.max_soc > 0) {
           gd* csoc = A(L.csoc); gd* dsoc = A(L.dsoc);
           const gd* ct = A(L.ct); const gd* dtv = A(L.dt);

@@ -151,7 +151,9 @@ class OrchardGeometryEnvironment(object):
 
     def check_path_feasibility(self, car_model, path, boundary_check=True, aux_check=False):
         """:423-458 (nearest-then-intersects == any intersects)."""
-        body, aux = car_model.get_path_poly(np.asarray(path, dtype=np.float64).reshape(-1, 3))
+        path = np.asarray(path, dtype=np.float64)
+        path = path.reshape(-1, path.shape[-1])[:, :3]
+        body, aux = car_model.get_path_poly(path)
         for poly in self.obs_poly_list:
             if convex_intersects(body, ring_of(poly)).any():
                 return False

@@ -67,7 +67,8 @@ class ReferenceLineHeuristic(object):
 
     def check_path_feasibility(self, car_model, path):
         """reference_line_heuristic.py:105-118: guided_lane contains the footprint union."""
-        body, _ = car_model.get_path_poly(np.asarray(path))
+        path = np.asarray(path, dtype=np.float64)
+        body, _ = car_model.get_path_poly(path.reshape(-1, path.shape[-1])[:, :3])
         return bool(union_contains([ring_of(s) for s in self.segment_lanes], body).all())
 
     def get_search_length(self, pose):
