@@ -52,6 +52,21 @@ class HaResult(ctypes.Structure):
                                                "dir", "k", "expanded")]
 
 
+class YpBatch(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("batch", "npoly", "nvert", "naxis")] + \
+        [(n, ctypes.c_void_p) for n in ("params", "desc", "poly_off", "vertices", "axis")] + [("cap_path", ctypes.c_int32)]
+
+
+class YpResult(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("status", "cand", "n_path", "params", "n_pose", "path")]
+
+
+YP_NPARAM, YP_NDESC = 16, 12
+(YP_P_EX, YP_P_EY, YP_P_EYAW, YP_P_BDIR, YP_P_FDIR, YP_P_WB, YP_P_STEP, YP_P_R00, YP_P_R01, YP_P_R10, YP_P_R11,
+ YP_P_TX, YP_P_TY, YP_P_YAW_ODOM) = range(14)
+YP_STATUS = {0: "found", 1: "none", 2: "end_blocked", 3: "bad_input"}
+YP_STATUS_BY_NAME = {v: k for k, v in YP_STATUS.items()}
+
 HA_NPARAM, HA_NDESC = 16, 12
 (HA_P_SX, HA_P_SY, HA_P_SYAW, HA_P_GX, HA_P_GY, HA_P_GYAW, HA_P_RES, HA_P_YAWRES, HA_P_WB, HA_P_MAXSTEER,
  HA_P_CURV, HA_P_DEFLEN, HA_P_MAXNODES) = range(13)
@@ -67,7 +82,8 @@ RS_SEG = "LSR"  # HTP_RS_SEG_L / _S / _R
 EXPORTS = ["htp_obca_sizes", "htp_create", "htp_destroy", "htp_last_error", "htp_set_option",
            "htp_obca_solve_batch", "htp_obca_solve_batch_device", "htp_last_kernel_ms", "htp_last_cycles",
            "htp_rs_all_paths_batch", "htp_rs_all_paths_batch_device", "htp_rs_last_ms",
-           "htp_hastar_search_batch", "htp_hastar_search_batch_device", "htp_hastar_last_ms"]
+           "htp_hastar_search_batch", "htp_hastar_search_batch_device", "htp_hastar_last_ms",
+           "htp_ypark_search_batch", "htp_ypark_search_batch_device", "htp_ypark_last_ms"]
 
 
 def _declare(lib):
@@ -104,6 +120,13 @@ def _declare(lib):
     lib.htp_hastar_search_batch_device.restype = ctypes.c_int
     lib.htp_hastar_last_ms.argtypes = [ctypes.c_void_p]
     lib.htp_hastar_last_ms.restype = ctypes.c_double
+    lib.htp_ypark_search_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(YpBatch), ctypes.POINTER(YpResult)]
+    lib.htp_ypark_search_batch.restype = ctypes.c_int
+    lib.htp_ypark_search_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(YpBatch), ctypes.POINTER(YpResult),
+                                                  ctypes.c_void_p]
+    lib.htp_ypark_search_batch_device.restype = ctypes.c_int
+    lib.htp_ypark_last_ms.argtypes = [ctypes.c_void_p]
+    lib.htp_ypark_last_ms.restype = ctypes.c_double
     return lib
 
 
@@ -352,6 +375,69 @@ class HastarResults:
         return [tuple(int(v) for v in r) for r in self.expanded[b, :n]]
 
 
+class YparkPacked:
+    """htp_ypark_batch pools for lowered Y-park searches (dicts made by
+    path_planner.headland_path_planning.lower_ypark)."""
+
+    def __init__(self, probs, cap_path=256):
+        B = len(probs)
+        polys, axis = [], []
+        self.params = np.zeros((B, YP_NPARAM))
+        self.desc = np.zeros((B, YP_NDESC), dtype=np.int32)
+        for b, p in enumerate(probs):
+            d = self.desc[b]
+            d[0] = len(polys)
+            polys.append(_clean_ring(p["body"]))
+            d[1] = len(polys)
+            for q in p["blockers"]:
+                polys.append(_clean_ring(q))
+            d[2] = len(polys)
+            if p["field"] is None:
+                d[3] = -1
+            else:
+                d[3] = len(polys)
+                polys.append(_clean_ring(p["field"]))
+            for a, key in enumerate(("backward_lengths", "forward_lengths", "backward_steers", "forward_steers")):
+                vals = np.asarray(p[key], dtype=np.float64).reshape(-1)
+                d[4 + 2 * a], d[5 + 2 * a] = len(axis), vals.size
+                axis.extend(vals.tolist())
+            self.params[b, :14] = [p["end_pose"][0], p["end_pose"][1], p["end_pose"][2], p["backward_steer_dir"],
+                                   p["forward_steer_dir"], p["wheel_base"], p["step"], p["T"][0][0], p["T"][0][1],
+                                   p["T"][1][0], p["T"][1][1], p["T"][0][3], p["T"][1][3], p["yaw_odom"]]
+        self.batch = B
+        self.poly_off = np.zeros(len(polys) + 1, dtype=np.int32)
+        self.poly_off[1:] = np.cumsum([q.shape[0] for q in polys])
+        self.vertices = np.ascontiguousarray(np.concatenate(polys, axis=0))
+        self.axis = np.array(axis, dtype=np.float64)
+        self.cap_path = int(cap_path)
+
+    def struct(self, ptrs=None):
+        src = ptrs or {}
+        b = YpBatch()
+        b.batch, b.npoly, b.nvert, b.naxis = self.batch, len(self.poly_off) - 1, self.vertices.shape[0], self.axis.size
+        for n in ("params", "desc", "poly_off", "vertices", "axis"):
+            setattr(b, n, src[n] if n in src else getattr(self, n).ctypes.data)
+        b.cap_path = self.cap_path
+        return b
+
+
+class YparkResults:
+    def __init__(self, packed):
+        B = packed.batch
+        self.status = np.zeros(B, np.int32)
+        self.cand = np.zeros(B, np.int32)
+        self.n_path = np.zeros(B, np.int32)
+        self.params = np.zeros((B, 4))
+        self.n_pose = np.zeros(B, np.int64)
+        self.path = np.zeros((B, packed.cap_path, 5))
+
+    def struct(self):
+        r = YpResult()
+        for n in ("status", "cand", "n_path", "params", "n_pose", "path"):
+            setattr(r, n, getattr(self, n).ctypes.data)
+        return r
+
+
 class Context:
     """Owns one htp_ctx (device workspace)."""
 
@@ -455,6 +541,18 @@ class Context:
 
     def hastar_last_ms(self):
         return self.lib.htp_hastar_last_ms(self.ctx)
+
+    def ypark(self, packed):
+        """Y-park grid searches of a YparkPacked batch (host buffers, synchronous)."""
+        res = YparkResults(packed)
+        b, r = packed.struct(), res.struct()
+        rc = self.lib.htp_ypark_search_batch(self.ctx, ctypes.byref(b), ctypes.byref(r))
+        if rc != 0:
+            raise RuntimeError(f"[htp] htp_ypark_search_batch failed: {self.error()}")
+        return res
+
+    def ypark_last_ms(self):
+        return self.lib.htp_ypark_last_ms(self.ctx)
 
     def close(self):
         if self.ctx:

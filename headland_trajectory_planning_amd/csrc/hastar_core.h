@@ -123,52 +123,17 @@ struct Shared {
 HTP_HD inline double pymod(double x, double y) { return rs::pymod(x, y); }
 HTP_HD inline double angle_wrap(double a) { return pymod(a + PI, 2.0 * PI) - PI; }  // path_utils.angle_wrap
 
-template <class C>
-struct Search {
-  C& c;
-  const double* prm;
-  const int32_t* dsc;
+// Footprint predicates at one pose (car_model.get_path_poly :39-73 body at the
+// pose): blocker polygons (separating axes, closed sets: touching collides),
+// field polygon containment (all corners inside by crossing number, no proper
+// crossing of edges), containment in the union of the lane polygons (every
+// body edge covered by the union of its clip intervals; skipped when the lane
+// range is empty, as for orchard_geometry_environment.check_path_feasibility).
+struct Footprint {
   Geo g;
-  Work w;
-  Shared& sh;
-  int nb, nmot;
-  double res, yaw_res, wb, curv_max, maxsteer;
+  const double* body;  // [nb][2] car-frame vertices (LDS on the device)
+  int nb, blk0, blk1, field, lane0, lane1;
 
-  HTP_HD Search(C& c_, const double* p, const int32_t* d, const Geo& g_, const Work& w_, Shared& s)
-      : c(c_), prm(p), dsc(d), g(g_), w(w_), sh(s) {
-    res = prm[P_RES];
-    yaw_res = prm[P_YAWRES];
-    wb = prm[P_WB];
-    curv_max = prm[P_CURV];
-    maxsteer = prm[P_MAXSTEER];
-    nmot = dsc[D_MOT1] - dsc[D_MOT0];
-    const int b0 = g.poly_off[dsc[D_BODY]];
-    nb = g.poly_off[dsc[D_BODY] + 1] - b0;
-    for (int q = c.lane; q < 2 * nb; q += C::width) sh.body[q] = g.vert[2 * b0 + q];
-    c.sync();
-  }
-
-  // ------------------------------------------------------------ reductions
-  HTP_HD int any(int v) const { return c.isum(v ? 1 : 0) > 0; }
-  // (value, index) min with the smallest index on ties; result uniform.
-  HTP_HD void argmin(double& v, int& i) const {
-    if (C::width == 1) return;
-    sh.red_d[c.lane] = v;
-    sh.red_i[c.lane] = i;
-    c.sync();
-    double bv = sh.red_d[0];
-    int bi = sh.red_i[0];
-    for (int l = 1; l < C::width; ++l) {
-      const double ov = sh.red_d[l];
-      const int oi = sh.red_i[l];
-      if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-    }
-    c.sync();
-    v = bv;
-    i = bi;
-  }
-
-  // ------------------------------------------------------------ geometry
   HTP_HD bool sat_hit(const double* bx, const double* by, int p) const {
     const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
     const double* V = g.vert + 2 * o;
@@ -243,7 +208,7 @@ struct Search {
 
   // every body edge covered by the union of the lane polygons (CCW, convex)
   HTP_HD bool in_lanes(const double* bx, const double* by) const {
-    const int j0 = dsc[D_LANE0], j1 = dsc[D_LANE1];
+    const int j0 = lane0, j1 = lane1;
     for (int k = 0; k < nb; ++k) {
       const int k1 = (k + 1) == nb ? 0 : k + 1;
       const double Ax = bx[k], Ay = by[k], Bx = bx[k1], By = by[k1];
@@ -288,15 +253,66 @@ struct Search {
     const double cs = cos(yaw), sn = sin(yaw);
     double bx[MAXB], by[MAXB];
     for (int k = 0; k < nb; ++k) {
-      const double vx = sh.body[2 * k], vy = sh.body[2 * k + 1];
+      const double vx = body[2 * k], vy = body[2 * k + 1];
       bx[k] = cs * vx + (-sn) * vy + x;
       by[k] = sn * vx + cs * vy + y;
     }
-    for (int p = dsc[D_BLK0]; p < dsc[D_BLK1]; ++p)
+    for (int p = blk0; p < blk1; ++p)
       if (sat_hit(bx, by, p)) return true;
-    if (dsc[D_FIELD] >= 0 && !in_field(bx, by, dsc[D_FIELD])) return true;
-    if (!in_lanes(bx, by)) return true;
+    if (field >= 0 && !in_field(bx, by, field)) return true;
+    if (lane1 > lane0 && !in_lanes(bx, by)) return true;
     return false;
+  }
+
+};
+
+template <class C>
+struct Search {
+  C& c;
+  const double* prm;
+  const int32_t* dsc;
+  Geo g;
+  Work w;
+  Shared& sh;
+  int nb, nmot;
+  double res, yaw_res, wb, curv_max, maxsteer;
+  Footprint fp;
+
+  HTP_HD Search(C& c_, const double* p, const int32_t* d, const Geo& g_, const Work& w_, Shared& s)
+      : c(c_), prm(p), dsc(d), g(g_), w(w_), sh(s) {
+    res = prm[P_RES];
+    yaw_res = prm[P_YAWRES];
+    wb = prm[P_WB];
+    curv_max = prm[P_CURV];
+    maxsteer = prm[P_MAXSTEER];
+    nmot = dsc[D_MOT1] - dsc[D_MOT0];
+    const int b0 = g.poly_off[dsc[D_BODY]];
+    nb = g.poly_off[dsc[D_BODY] + 1] - b0;
+    for (int q = c.lane; q < 2 * nb; q += C::width) sh.body[q] = g.vert[2 * b0 + q];
+    c.sync();
+    fp = Footprint{g, sh.body, nb, dsc[D_BLK0], dsc[D_BLK1], dsc[D_FIELD], dsc[D_LANE0], dsc[D_LANE1]};
+  }
+
+  HTP_HD bool pose_hits(double x, double y, double yaw) const { return fp.pose_hits(x, y, yaw); }
+
+  // ------------------------------------------------------------ reductions
+  HTP_HD int any(int v) const { return c.isum(v ? 1 : 0) > 0; }
+  // (value, index) min with the smallest index on ties; result uniform.
+  HTP_HD void argmin(double& v, int& i) const {
+    if (C::width == 1) return;
+    sh.red_d[c.lane] = v;
+    sh.red_i[c.lane] = i;
+    c.sync();
+    double bv = sh.red_d[0];
+    int bi = sh.red_i[0];
+    for (int l = 1; l < C::width; ++l) {
+      const double ov = sh.red_d[l];
+      const int oi = sh.red_i[l];
+      if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    c.sync();
+    v = bv;
+    i = bi;
   }
 
   // ------------------------------------------------------------ heuristic

@@ -27,6 +27,10 @@ struct htp_ctx {
   void* ha_ws = nullptr;
   size_t ha_ws_bytes = 0;
   hipEvent_t ha_ev0 = nullptr, ha_ev1 = nullptr;
+  // Y-park batch (htp_ypark.hip)
+  void* yp_ws = nullptr;
+  size_t yp_ws_bytes = 0;
+  hipEvent_t yp_ev0 = nullptr, yp_ev1 = nullptr;
 };
 
 static inline int fail(htp_ctx* c, const std::string& m) {

@@ -93,6 +93,8 @@ htp_ctx* htp_create(int32_t device) {
   (void)hipEventCreate(&c->rs_ev1);
   (void)hipEventCreate(&c->ha_ev0);
   (void)hipEventCreate(&c->ha_ev1);
+  (void)hipEventCreate(&c->yp_ev0);
+  (void)hipEventCreate(&c->yp_ev1);
   return c;
 }
 
@@ -109,6 +111,9 @@ void htp_destroy(htp_ctx* c) {
   if (c->ha_ws) (void)hipFree(c->ha_ws);
   if (c->ha_ev0) (void)hipEventDestroy(c->ha_ev0);
   if (c->ha_ev1) (void)hipEventDestroy(c->ha_ev1);
+  if (c->yp_ws) (void)hipFree(c->yp_ws);
+  if (c->yp_ev0) (void)hipEventDestroy(c->yp_ev0);
+  if (c->yp_ev1) (void)hipEventDestroy(c->yp_ev1);
   delete c;
 }
 

@@ -7,9 +7,10 @@ import math
 
 import numpy as np
 
+from .. import _native
 from ..obca_py.util import calc_spline_course
 from . import transformation as trans
-from .geom import angle_wrap
+from .geom import angle_wrap, ring_of
 from .hybrid_a_star_search import HybridAStarSearch
 from .navigation_utils import convert_2d_xys_to_target_frame
 from .reference_line_heuristic import ReferenceLineHeuristic
@@ -105,35 +106,80 @@ def y_park_grid(max_steer_backward, max_steer_forward, max_backward_distance, ma
     return bl, fl, sb, sf
 
 
+def lower_ypark(car_model, config_env, end_pose, backward_steer_dir, forward_steer_dir, max_steer_backward=0.4,
+                max_steer_forward=0.45, max_backward_distance=3.5, max_forward_distance=2.0,
+                min_forward_distance=1.4, min_backward_distance=0.7, min_steer_backward=0.3,
+                min_steer_forward=0.3, step_size=0.1):
+    """Flat description of one search_y_type_parking_path call (input of _native.YparkPacked)."""
+    bl, fl, sb, sf = y_park_grid(max_steer_backward, max_steer_forward, max_backward_distance, max_forward_distance,
+                                 min_forward_distance, min_backward_distance, min_steer_backward, min_steer_forward)
+    T = trans.states2SE3([end_pose[0], end_pose[1], 0, 0, 0, end_pose[2]])
+    return dict(end_pose=np.asarray(end_pose, dtype=np.float64)[:3], backward_steer_dir=float(backward_steer_dir),
+                forward_steer_dir=float(forward_steer_dir), wheel_base=float(car_model.WHEEL_BASE),
+                step=float(step_size), T=T, yaw_odom=float(trans.SE32states(T)[-1]),
+                backward_lengths=np.asarray(bl, dtype=np.float64), forward_lengths=np.asarray(fl, dtype=np.float64),
+                backward_steers=np.asarray(sb, dtype=np.float64), forward_steers=np.asarray(sf, dtype=np.float64),
+                body=ring_of(car_model.car_poly), blockers=[ring_of(q) for q in config_env.obs_poly_list],
+                field=ring_of(config_env.field_range_poly))
+
+
+_CTX = None
+
+
+def search_y_lowered(problems, ctx=None):
+    """Run lowered Y-park searches on the GPU -> list of dicts (status, params, path)."""
+    global _CTX
+    if ctx is None:
+        if _CTX is None:
+            _CTX = _native.Context(0)
+        ctx = _CTX
+    res = ctx.ypark(_native.YparkPacked(problems))
+    out = []
+    for b in range(len(problems)):
+        n = int(res.n_path[b])
+        out.append(dict(status=int(res.status[b]), cand=int(res.cand[b]), params=res.params[b].tolist(),
+                        path=res.path[b, :n].copy(), n_pose=int(res.n_pose[b])))
+    return out
+
+
+def _report_ypark(r, debug):
+    if r["status"] == _native.YP_STATUS_BY_NAME["end_blocked"]:
+        print(" [Y-type Planner] The end pose is interfered with the environment!")
+        return [], []
+    if r["status"] == _native.YP_STATUS_BY_NAME["bad_input"]:
+        raise ValueError("[Y-type Planner] grid outside the kernel's limits (<= 63 poses per arc)")
+    if r["status"] != _native.YP_STATUS_BY_NAME["found"]:
+        return ([], []) if debug else []
+    bl, fl, sb, sf = r["params"]
+    print("backward distance:%.2f, forward distance:%.2f, backward steer:%.2f, forward steer:%.2f,  "
+          % (bl, fl, sb, sf))
+    return (r["path"], [bl, fl, sb, sf]) if debug else r["path"]
+
+
 def search_y_type_parking_path(car_model, config_env, end_pose, backward_steer_dir, forward_steer_dir,
                                max_steer_backward=0.4, max_steer_forward=0.45, max_backward_distance=3.5,
                                max_forward_distance=2.0, min_forward_distance=1.4, min_backward_distance=0.7,
                                min_steer_backward=0.3, min_steer_forward=0.3, step_size=0.1, debug=False):
     """:382-451: first feasible (backward length, forward length, backward steer,
-    forward steer) in lexicographic loop order."""
-    if not config_env.check_path_feasibility(car_model, np.array([end_pose])):
-        print(" [Y-type Planner] The end pose is interfered with the environment!")
-        return [], []
-    bl, fl, sb, sf = y_park_grid(max_steer_backward, max_steer_forward, max_backward_distance, max_forward_distance,
-                                 min_forward_distance, min_backward_distance, min_steer_backward, min_steer_forward)
-    T = trans.states2SE3([end_pose[0], end_pose[1], 0, 0, 0, end_pose[2]])
-    for backward_length in bl:
-        for forward_length in fl:
-            for steer_backward in sb:
-                for steer_forward in sf:
-                    p = get_y_type_parking_path(car_model, backward_length, steer_backward * backward_steer_dir,
-                                                forward_length, steer_forward * forward_steer_dir, step_size)
-                    p = get_path_in_odom(T, p)
-                    if config_env.check_path_feasibility(car_model, p):
-                        print("backward distance:%.2f, forward distance:%.2f, backward steer:%.2f, "
-                              "forward steer:%.2f,  " % (backward_length, forward_length, steer_backward,
-                                                         steer_forward))
-                        if debug:
-                            return p, [backward_length, forward_length, steer_backward, steer_forward]
-                        return p
-    if debug:
-        return [], []
-    return []
+    forward steer) in lexicographic loop order, searched on the GPU
+    (htp_ypark_search_batch)."""
+    prob = lower_ypark(car_model, config_env, end_pose, backward_steer_dir, forward_steer_dir, max_steer_backward,
+                       max_steer_forward, max_backward_distance, max_forward_distance, min_forward_distance,
+                       min_backward_distance, min_steer_backward, min_steer_forward, step_size)
+    # an interfering end pose gives ([], []) regardless of debug, like the reference (:400-402)
+    return _report_ypark(search_y_lowered([prob])[0], debug)
+
+
+def search_y_type_parking_path_batch(searches, ctx=None):
+    """Many searches in one launch: `searches` are keyword dicts of
+    search_y_type_parking_path's arguments; returns [(path, [bl, fl, sb, sf])]
+    with ([], []) where none is feasible."""
+    probs = [lower_ypark(**{k: v for k, v in s.items() if k != "debug"}) for s in searches]
+    out = []
+    for r in search_y_lowered(probs, ctx):
+        ok = r["status"] == _native.YP_STATUS_BY_NAME["found"]
+        out.append((r["path"], list(r["params"])) if ok else ([], []))
+    return out
 
 
 def calculate_motion_path(init_pose, motion_command, search_length, wheel_base, step):

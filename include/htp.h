@@ -222,6 +222,56 @@ int htp_hastar_search_batch_device(htp_ctx* ctx, const htp_hastar_batch* in, htp
 /* Duration (ms) of the last search kernel (hipEvents on its stream). */
 double htp_hastar_last_ms(htp_ctx* ctx);
 
+
+/* ---------------------------------------------------------------------------
+ * Y-type parking grid search: search_y_type_parking_path(car_model, config_env,
+ * end_pose, backward_steer_dir, forward_steer_dir, max/min steers and lengths,
+ * step_size) R/path_planner/headland_path_planning.py:382-451, one search per
+ * problem of the batch.  The grid axes (np.arange values, the reference's loop
+ * order: backward length, forward length, backward steer, forward steer) live in
+ * `axis`; the first collision-free candidate is returned with its manoeuvre
+ * (rows x, y, yaw, k, dir in the odom frame, get_y_type_parking_path +
+ * get_path_in_odom :487-527).  Footprint = car_poly at every pose against
+ * blockers (obstacle + tree polygons) and inside the field polygon
+ * (check_path_feasibility :423-458, boundary_check=True). */
+#define HTP_YP_NPARAM 16
+enum {
+  HTP_YP_P_EX = 0, HTP_YP_P_EY, HTP_YP_P_EYAW,  /* end (row-enter) pose */
+  HTP_YP_P_BDIR, HTP_YP_P_FDIR,                 /* backward / forward steer directions (+-1) */
+  HTP_YP_P_WB, HTP_YP_P_STEP,                   /* car_model.WHEEL_BASE, step_size */
+  HTP_YP_P_R00, HTP_YP_P_R01, HTP_YP_P_R10, HTP_YP_P_R11, HTP_YP_P_TX, HTP_YP_P_TY,  /* states2SE3(end pose) */
+  HTP_YP_P_YAW_ODOM                             /* SE32states(T)[5] */
+};
+#define HTP_YP_NDESC 12
+enum {
+  HTP_YP_D_BODY = 0, HTP_YP_D_BLK0, HTP_YP_D_BLK1, HTP_YP_D_FIELD,
+  HTP_YP_D_BL0, HTP_YP_D_NBL, HTP_YP_D_FL0, HTP_YP_D_NFL, HTP_YP_D_SB0, HTP_YP_D_NSB, HTP_YP_D_SF0, HTP_YP_D_NSF
+};
+enum { HTP_YP_FOUND = 0, HTP_YP_NONE = 1, HTP_YP_END_BLOCKED = 2, HTP_YP_BAD_INPUT = 3 };
+
+typedef struct {
+  int32_t batch, npoly, nvert, naxis;
+  const double* params;     /* [batch][HTP_YP_NPARAM] */
+  const int32_t* desc;      /* [batch][HTP_YP_NDESC] */
+  const int32_t* poly_off;  /* [npoly+1] */
+  const double* vertices;   /* [nvert][2] */
+  const double* axis;       /* [naxis] grid axis values */
+  int32_t cap_path;         /* rows per search in `path` */
+} htp_ypark_batch;
+
+typedef struct {
+  int32_t* status;   /* [batch] HTP_YP_* */
+  int32_t* cand;     /* [batch] index of the chosen candidate in loop order (-1: none) */
+  int32_t* n_path;   /* [batch] rows of the chosen manoeuvre */
+  double* params;    /* [batch][4] backward length, forward length, backward steer, forward steer */
+  int64_t* n_pose;   /* [batch] footprint poses tested (nullable) */
+  double* path;      /* [batch][cap_path][5] */
+} htp_ypark_result;
+
+int htp_ypark_search_batch(htp_ctx* ctx, const htp_ypark_batch* in, htp_ypark_result* out);
+int htp_ypark_search_batch_device(htp_ctx* ctx, const htp_ypark_batch* in, htp_ypark_result* out, void* stream);
+double htp_ypark_last_ms(htp_ctx* ctx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,7 +22,7 @@ def build():
         return SO
     subprocess.check_call(["g++", "-O2", "-fno-builtin", "-std=c++17", "-shared", "-fPIC", "-o", SO,
                            os.path.join(CSRC, "htp_hostsim.cpp"), os.path.join(CSRC, "rs_hostsim.cpp"),
-                           os.path.join(CSRC, "hastar_hostsim.cpp")])
+                           os.path.join(CSRC, "hastar_hostsim.cpp"), os.path.join(CSRC, "ypark_hostsim.cpp")])
     return SO
 
 
@@ -130,3 +130,22 @@ def as_dicts(res):
         out.append(dict(xs=xs, ys=ys, yaws=yaws, dirs=dirs, ks=ks, counter=int(res.counter[b]),
                         status=int(res.status[b]), expanded=res.expansions(b), n_pose=int(res.n_pose[b])))
     return out
+
+
+def ypark_host(problems, cap_path=256):
+    """Host build of csrc/ypark_core.h (serial lane), same result object as
+    Context.ypark.  TEST-ONLY."""
+    l = lib()
+    f = l.htp_hostsim_ypark
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.POINTER(_native.YpBatch), ctypes.POINTER(_native.YpResult)]
+    pk = _native.YparkPacked(problems, cap_path=cap_path)
+    res = _native.YparkResults(pk)
+    assert f(ctypes.byref(pk.struct()), ctypes.byref(res.struct())) == 0
+    return res
+
+
+def ypark_dicts(res):
+    return [dict(status=int(res.status[b]), cand=int(res.cand[b]), params=res.params[b].tolist(),
+                 path=res.path[b, :int(res.n_path[b])].copy(), n_pose=int(res.n_pose[b]))
+            for b in range(len(res.status))]

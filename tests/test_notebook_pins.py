@@ -19,9 +19,13 @@ def _host_hastar(problems, ctx=None, cap_path=4096):
     return H.as_dicts(H.hastar_host(problems, cap_path=cap_path))
 
 
+def _host_ypark(problems, ctx=None):
+    return H.ypark_dicts(H.ypark_host(problems))
+
+
 @pytest.fixture(scope="module")
 def ws():
-    return NB.warm_start(_host_hastar)
+    return NB.warm_start(_host_hastar, _host_ypark)
 
 
 def test_warm_start_reproduces_notebook_prints(ws):
