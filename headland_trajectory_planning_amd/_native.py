@@ -288,8 +288,6 @@ class HastarPacked:
         self.desc = np.zeros((B, HA_NDESC), dtype=np.int32)
         ng = nm = 0
         for b, p in enumerate(probs):
-            if not p.get("king", True):
-                raise NotImplementedError("[HA*] motion_type 'Pawn' (Dubins goal shots) is not supported by the kernel")
             d = self.desc[b]
             d[HA_D_BODY] = len(polys)
             polys.append(_clean_ring(p["body"]))
@@ -318,7 +316,7 @@ class HastarPacked:
             d[HA_D_MOT0], d[HA_D_MOT1] = nm, nm + m.shape[0]
             motions.append(m)
             nm += m.shape[0]
-            d[HA_D_KING] = 1
+            d[HA_D_KING] = 1 if p.get("king", True) else 0
             pr = self.params[b]
             pr[HA_P_SX:HA_P_SYAW + 1] = np.asarray(p["start"], dtype=np.float64)[:3]
             pr[HA_P_GX:HA_P_GYAW + 1] = np.asarray(p["goal"], dtype=np.float64)[:3]

@@ -28,7 +28,11 @@
 #pragma once
 #include <cmath>
 #include <cstdint>
+#ifdef HTP_HA_DEBUG
+#include <cstdio>
+#endif
 
+#include "dubins_core.h"
 #include "rs_core.h"
 
 #if defined(__clang__)
@@ -57,7 +61,7 @@ enum {
 };
 // search status (htp.h HTP_HA_*)
 enum { ST_FOUND = 0, ST_NO_PATH = 1, ST_MAX_NODES = 2, ST_START_GOAL_BLOCKED = 3, ST_RS_ERROR = 4,
-       ST_CAPACITY = 5, ST_BAD_INPUT = 6, ST_BACKTRACK = 7 };
+       ST_CAPACITY = 5, ST_BAD_INPUT = 6, ST_BACKTRACK = 7 };  // ST_CAPACITY also: Dubins shot beyond cap_dub
 
 struct Geo {
   const int32_t* poly_off;  // [npoly+1] vertex ranges
@@ -72,7 +76,7 @@ struct Node {  // 64 B
   int32_t kx, ky, kt;       // grid index
   int32_t pkx, pky, pkt;    // parent grid index
   int32_t parent;           // node id of the expanding node (-1: start)
-  int16_t kind;             // 0 start, 1 motion, 2 Reeds-Shepp goal shot
+  int16_t kind;             // 0 start, 1 motion, 2 Reeds-Shepp goal shot, 3 Dubins goal shot
   int16_t aux;              // motion index / RS path index
   int32_t dir;
 };
@@ -90,7 +94,11 @@ struct Work {  // per-search HBM workspace
   double* hval;
   int32_t* hslot;
   int32_t cap_node, cap_slot;  // cap_slot: power of two
+  double* dub;                 // Pawn goal shot scratch: DUBW * (cap_dub + 16) doubles
+  int32_t cap_dub;             // Dubins samples per shot
 };
+constexpr int DUBW = 16;       // X Y S DX DY | work 4 + 4 | XS YS YAW
+constexpr int CAP_DUB = 4096;  // Dubins samples per Pawn goal shot (409.6 m at res 0.1)
 
 struct Out {
   int32_t status, counter, n_path, n_expanded;
@@ -676,6 +684,136 @@ struct Search {
     return -1;
   }
 
+  // ------------------------------------------------------------ Dubins goal shot (Pawn)
+  // get_dubins_path :289-304 for the pose (x0, y0, yaw0): Dubins samples + goal,
+  // arc-length spline fit.  Leaves X, Y, S, DX, DY (m points) in w.dub; returns
+  // the number of spline samples (np.arange(0, s_end + ds, ds)), -1 on overflow.
+  HTP_HD int dubins_fit(double x0, double y0, double yaw0, int& m) {
+    const int cap = w.cap_dub + 16;
+    double* X = w.dub;
+    double* Y = X + cap;
+    double* S = Y + cap;
+    double* DX = S + cap;
+    double* DY = DX + cap;
+    double* WK = DY + cap;
+    const double q0[3] = {x0, y0, yaw0}, q1[3] = {prm[P_GX], prm[P_GY], prm[P_GYAW]};
+    dub::Path P;
+    if (!dub::shortest(q0, q1, 1.0 / curv_max, P)) {
+#ifdef HTP_HA_DEBUG
+      if (c.lane == 0) printf("dub shortest fail %.17g %.17g %.17g\n", x0, y0, yaw0);
+#endif
+      return -1;
+    }
+    const double L = dub::length(P);
+    int n = 0;
+    double xs = 0.0;
+    while (xs < L) {  // sample_many: x = 0, step, 2 step ... (sequential sums)
+      if (n >= w.cap_dub) {
+#ifdef HTP_HA_DEBUG
+        if (c.lane == 0) printf("dub n overflow L=%.17g\n", L);
+#endif
+        return -1;
+      }
+      S[n] = xs;
+      ++n;
+      xs += res;
+    }
+    c.sync();
+    for (int k = c.lane; k < n; k += C::width) {
+      double q[3];
+      dub::sample(P, S[k], q);
+      X[k] = q[0];
+      Y[k] = q[1];
+    }
+    c.sync();
+    X[n] = q1[0];  // uniform: every lane stores the same value
+    Y[n] = q1[1];
+    c.sync();
+    // drop point i when point i+1 repeats it (cubic_spline.py:94-99), then s
+    int mm = 0;
+    for (int i = 0; i <= n; ++i) {
+      const bool dup = i < n && X[i + 1] == X[i] && Y[i + 1] == Y[i];
+      if (!dup) {  // uniform: every lane moves the same values
+        const double xi = X[i], yi = Y[i];
+        X[mm] = xi;
+        Y[mm] = yi;
+        ++mm;
+      }
+    }
+    c.sync();
+    S[0] = 0.0;
+    for (int i = 1; i < mm; ++i) S[i] = S[i - 1] + hypot(X[i] - X[i - 1], Y[i] - Y[i - 1]);
+    c.sync();
+    m = mm;
+#ifdef HTP_HA_DEBUG
+    if (c.lane == 0) printf("dub fit L=%.17g n=%d m=%d S=%.17g\n", L, n, mm, S[mm - 1]);
+#endif
+    if (m < 2) return -1;
+    if (c.lane == 0 || C::width == 1) dub::spline_slopes(S, X, m, DX, WK);
+    if (c.lane == (C::width > 1 ? 1 : 0)) dub::spline_slopes(S, Y, m, DY, WK + 4 * cap);
+    c.sync();
+    const double ns = ceil((S[m - 1] + res) / res);
+    if (!(ns >= 1) || ns > (double)w.cap_dub) {
+#ifdef HTP_HA_DEBUG
+      if (c.lane == 0) printf("dub ns bad %.17g\n", ns);
+#endif
+      return -1;
+    }
+    return (int)ns;
+  }
+
+  // spline sample k: x, y, yaw (not wrapped), curvature
+  HTP_HD void dubins_eval(int k, int m, double& x, double& y, double& yaw, double& kap) const {
+    const int cap = w.cap_dub + 16;
+    const double* X = w.dub;
+    const double* Y = X + cap;
+    const double* S = Y + cap;
+    const double* DX = S + cap;
+    const double* DY = DX + cap;
+    const double v = (double)k * res;
+    const int i = dub::interval(S, m, v);
+    double x1, x2, y1, y2;
+    dub::eval3(S, X, DX, i, v, x, x1, x2);
+    dub::eval3(S, Y, DY, i, v, y, y1, y2);
+    yaw = atan2(y1, x1);
+    kap = (y2 * x1 - x2 * y1) / pow(x1 * x1 + y1 * y1, 1.5);
+  }
+
+  // _get_goal_extension_with_dubins_path :184-230: true if the shot is taken
+  HTP_HD bool goal_shot_dubins(const Node& cur, int& err, int64_t& n_pose, int64_t& n_checks) {
+    int m = 0;
+    const int ns = dubins_fit(cur.x, cur.y, cur.yaw, m);
+    if (ns < 0) { err = 1; return false; }
+    const int cap = w.cap_dub + 16;
+    double* XS = w.dub + 13 * cap;
+    double* YS = XS + cap;
+    double* YW = YS + cap;
+    for (int k = c.lane; k < ns; k += C::width) {
+      double x, y, yaw, kap;
+      dubins_eval(k, m, x, y, yaw, kap);
+      XS[k] = x;
+      YS[k] = y;
+      YW[k] = angle_wrap(yaw);
+    }
+    c.sync();
+    // calculate_path_length: cumsum of hypot(diff) (sequential)
+    double len = 0.0;
+    for (int k = 1; k < ns; ++k) {
+      const double h = hypot(XS[k] - XS[k - 1], YS[k] - YS[k - 1]);
+      len = (k == 1) ? h : len + h;
+    }
+    if (!(len < 1000.0)) return false;  // path_length < MIN_LENGTH_TO_GOAL (checked first: same outcome)
+    ++n_checks;
+    for (int base = 0; base < ns; base += 64) {  // collision, 64 samples at a time, early exit
+      int h = 0;
+      for (int k = base + c.lane; k < base + 64 && k < ns; k += C::width)
+        if (pose_hits(XS[k], YS[k], YW[k])) h = 1;
+      n_pose += (ns - base) < 64 ? (ns - base) : 64;
+      if (any(h)) return false;
+    }
+    return true;
+  }
+
   HTP_HD bool traj_hits_single(double x, double y, double yaw, int64_t& n_pose) {
     int h = 0;
     if (c.lane == 0) h = pose_hits(x, y, yaw) ? 1 : 0;
@@ -689,7 +827,16 @@ struct Search {
     return nn++;
   }
 
+  // KING: Reeds-Shepp goal shots (motion_type "King"); otherwise Dubins (Pawn).
+  // The device instantiates one kernel per motion type, so neither carries the
+  // other's goal-shot code (register pressure).
   HTP_HD void run(Out& o, int32_t* log, int cap_log) {
+    if (dsc[D_KING]) run_t<true>(o, log, cap_log);
+    else run_t<false>(o, log, cap_log);
+  }
+
+  template <bool KING>
+  HTP_HD void run_t(Out& o, int32_t* log, int cap_log) {
     o = Out{};
     const int max_nodes = (int)prm[P_MAXNODES];
     for (int q = c.lane; q < w.cap_slot; q += C::width) {
@@ -744,8 +891,15 @@ struct Search {
       // goal extension
       int err = 0;
       double gcost = 0.0;
-      const int pk = goal_shot(cur, gcost, err, o.n_pose, o.n_checks);
-      if (err) { status = ST_RS_ERROR; break; }
+      int pk = -1;
+      if constexpr (KING) {
+        pk = goal_shot(cur, gcost, err, o.n_pose, o.n_checks);
+        if (err) { status = ST_RS_ERROR; break; }
+      } else {
+        const bool shot = goal_shot_dubins(cur, err, o.n_pose, o.n_checks);
+        if (err) { status = ST_CAPACITY; break; }
+        pk = shot ? 0 : -1;
+      }
       int gid = -1;
       if (pk >= 0) {
         gid = new_node(nn);
@@ -753,7 +907,8 @@ struct Search {
         Node gn{};
         gn.x = prm[P_GX]; gn.y = prm[P_GY]; gn.yaw = prm[P_GYAW];  // end pose (unused: never expanded)
         gn.cost = gcost; gn.curv = 0.0; gn.kx = gk[0]; gn.ky = gk[1]; gn.kt = gk[2];
-        gn.pkx = cur.kx; gn.pky = cur.ky; gn.pkt = cur.kt; gn.parent = cid; gn.kind = 2; gn.aux = (int16_t)pk;
+        gn.pkx = cur.kx; gn.pky = cur.ky; gn.pkt = cur.kt; gn.parent = cid; gn.kind = KING ? 2 : 3;
+        gn.aux = (int16_t)pk;
         gn.dir = 1;
         if (c.lane == 0 || C::width == 1) w.node[gid] = gn;
       }
@@ -845,6 +1000,13 @@ struct Search {
   // get_path_from_expanded_nodes :429-454 -> number of samples written (or needed)
   HTP_HD int backtrack(int32_t* chain, int cap_chain, double* px, double* py, double* pyaw, double* pdir,
                        double* pk, int cap_path, int& status) {
+    return dsc[D_KING] ? backtrack_t<true>(chain, cap_chain, px, py, pyaw, pdir, pk, cap_path, status)
+                       : backtrack_t<false>(chain, cap_chain, px, py, pyaw, pdir, pk, cap_path, status);
+  }
+
+  template <bool KING>
+  HTP_HD int backtrack_t(int32_t* chain, int cap_chain, double* px, double* py, double* pyaw, double* pdir,
+                         double* pk, int cap_path, int& status) {
     // the start node is node 0; its grid index is the goal's if the start itself
     // arrived (check_the_arrival relabels the node object, :492-493)
     const int32_t sk[3] = {w.node[0].kx, w.node[0].ky, w.node[0].kt};
@@ -888,6 +1050,18 @@ struct Search {
             pdir[off + i] = dir; pk[off + i] = kv;
           }
         off += n + 1;
+        c.sync();
+      } else if constexpr (!KING) {
+        const Node par = w.node[nd.parent];
+        int m = 0;
+        const int ns = dubins_fit(par.x, par.y, par.yaw, m);
+        for (int k = c.lane; k < ns; k += C::width)
+          if (off + k < cap_path) {
+            double x, y, yaw, kap;
+            dubins_eval(k, m, x, y, yaw, kap);
+            px[off + k] = x; py[off + k] = y; pyaw[off + k] = angle_wrap(yaw); pdir[off + k] = 1.0; pk[off + k] = kap;
+          }
+        off += ns > 0 ? ns : 0;
         c.sync();
       } else {
         const Node par = w.node[nd.parent];

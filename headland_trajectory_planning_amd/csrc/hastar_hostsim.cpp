@@ -22,13 +22,14 @@ extern "C" int htp_hostsim_hastar(const htp_hastar_batch* in, htp_hastar_result*
   std::vector<Slot> slots((size_t)cs);
   std::vector<double> hval((size_t)cn);
   std::vector<int32_t> hslot((size_t)cn);
+  std::vector<double> dub((size_t)DUBW * (CAP_DUB + 16));
   Shared* sh = new Shared();
   Geo g{in->poly_off, in->vertices, in->lane_len, in->guide, in->motions};
   for (int b = 0; b < in->batch; ++b) {
     const double* prm = in->params + (int64_t)b * HTP_HA_NPARAM;
     const int32_t* d = in->desc + (int64_t)b * HTP_HA_NDESC;
     HostLane c;
-    Work w{nodes.data(), slots.data(), hval.data(), hslot.data(), (int32_t)cn, (int32_t)cs};
+    Work w{nodes.data(), slots.data(), hval.data(), hslot.data(), (int32_t)cn, (int32_t)cs, dub.data(), CAP_DUB};
     Search<HostLane> S(c, prm, d, g, w, *sh);
     Out o{};
     int32_t* log = out->expanded ? out->expanded + (int64_t)b * in->cap_log * 3 : nullptr;

@@ -37,7 +37,8 @@ Sizes ws_sizes(int max_nodes_cap) {
   while (cs < 2 * cn) cs <<= 1;
   z.cap_slot = (int32_t)cs;
   auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
-  z.per_search = al(sizeof(Node) * (size_t)cn) + al(sizeof(Slot) * (size_t)cs) + al(8 * (size_t)cn) + al(4 * (size_t)cn);
+  z.per_search = al(sizeof(Node) * (size_t)cn) + al(sizeof(Slot) * (size_t)cs) + al(8 * (size_t)cn) + al(4 * (size_t)cn) +
+                 al(8 * (size_t)DUBW * (CAP_DUB + 16));
   return z;
 }
 
@@ -48,9 +49,11 @@ HTP_HD inline Work work_of(char* base, const Sizes& z, int b) {
   w.node = (Node*)p; p += al(sizeof(Node) * (size_t)z.cap_node);
   w.slot = (Slot*)p; p += al(sizeof(Slot) * (size_t)z.cap_slot);
   w.hval = (double*)p; p += al(8 * (size_t)z.cap_node);
-  w.hslot = (int32_t*)p;
+  w.hslot = (int32_t*)p; p += al(4 * (size_t)z.cap_node);
+  w.dub = (double*)p;
   w.cap_node = z.cap_node;
   w.cap_slot = z.cap_slot;
+  w.cap_dub = CAP_DUB;
   return w;
 }
 
@@ -65,7 +68,7 @@ __device__ bool valid(const Pools& P, const double* prm, const int32_t* d, int m
   if (d[D_FIELD] != -1 && !poly_ok(d[D_FIELD])) return false;
   if (d[D_GUIDE0] < 0 || d[D_GUIDE1] <= d[D_GUIDE0] || d[D_GUIDE1] > P.nguide) return false;
   if (d[D_MOT0] < 0 || d[D_MOT1] <= d[D_MOT0] || d[D_MOT1] > P.nmotion || d[D_MOT1] - d[D_MOT0] > MAXMOT) return false;
-  if (d[D_KING] != 1) return false;
+  if (d[D_KING] != 0 && d[D_KING] != 1) return false;
   for (int p = 0; p < P.npoly; ++p) (void)p;
   const double res = prm[P_RES];
   if (!(res > 0) || !(prm[P_YAWRES] > 0) || !(prm[P_WB] > 0) || !(prm[P_CURV] > 0)) return false;
@@ -83,14 +86,20 @@ __device__ bool valid(const Pools& P, const double* prm, const int32_t* d, int m
   return true;
 }
 
+// One instantiation per motion type (King: Reeds-Shepp goal shots, Pawn:
+// Dubins + spline); each launch covers the whole batch and a search is run by
+// the instantiation of its own type (searches with an invalid type by King's,
+// which reports them as bad input).
+template <bool KING>
 __global__ __launch_bounds__(64) void hastar_kernel(Pools P, int batch, int max_nodes_cap, char* ws, Sizes z,
                                                     htp_hastar_result out, int cap_path, int cap_log) {
   __shared__ Shared sh;
   const int b = blockIdx.x;
   if (b >= batch) return;
-  DevWave c{(int)threadIdx.x, nullptr, nullptr};
   const double* prm = P.params + (int64_t)b * HTP_HA_NPARAM;
   const int32_t* d = P.desc + (int64_t)b * HTP_HA_NDESC;
+  if ((d[D_KING] != 0) != KING) return;
+  DevWave c{(int)threadIdx.x, nullptr, nullptr};
   Out o{};
   int n_path = 0;
   if (!valid(P, prm, d, max_nodes_cap)) {
@@ -99,11 +108,11 @@ __global__ __launch_bounds__(64) void hastar_kernel(Pools P, int batch, int max_
     Work w = work_of(ws, z, b);
     Search<DevWave> S(c, prm, d, P.g, w, sh);
     int32_t* log = out.expanded ? out.expanded + (int64_t)b * cap_log * 3 : nullptr;
-    S.run(o, log, log ? cap_log : 0);
+    S.template run_t<KING>(o, log, log ? cap_log : 0);
     if (o.status == ST_FOUND || o.status == ST_NO_PATH || o.status == ST_MAX_NODES) {
       const int64_t off = (int64_t)b * cap_path;
       int st = o.status;
-      n_path = S.backtrack(w.hslot, w.cap_node, out.x + off, out.y + off, out.yaw + off, out.dir + off, out.k + off,
+      n_path = S.template backtrack_t<KING>(w.hslot, w.cap_node, out.x + off, out.y + off, out.yaw + off, out.dir + off, out.k + off,
                            cap_path, st);
       o.status = st;
     }
@@ -121,7 +130,10 @@ int enqueue(htp_ctx* ctx, const htp_hastar_batch* in, const Pools& P, htp_hastar
   const Sizes z = ws_sizes(in->max_nodes_cap);
   if (ensure(ctx, &ctx->ha_ws, &ctx->ha_ws_bytes, z.per_search * (size_t)in->batch)) return -1;
   HIPCHK(hipEventRecord(ctx->ha_ev0, s));
-  hipLaunchKernelGGL(hastar_kernel, dim3(in->batch), dim3(64), 0, s, P, in->batch, in->max_nodes_cap,
+  hipLaunchKernelGGL(hastar_kernel<true>, dim3(in->batch), dim3(64), 0, s, P, in->batch, in->max_nodes_cap,
+                     (char*)ctx->ha_ws, z, out, in->cap_path, out.expanded ? in->cap_log : 0);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(hastar_kernel<false>, dim3(in->batch), dim3(64), 0, s, P, in->batch, in->max_nodes_cap,
                      (char*)ctx->ha_ws, z, out, in->cap_path, out.expanded ? in->cap_log : 0);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ha_ev1, s));

@@ -14,8 +14,9 @@ Duck types read by the lowering (the reference's own objects work too):
   car_model           .car_poly, .WHEEL_BASE, .MAX_STEER (curvature = tan(MAX_STEER)/WHEEL_BASE, car_model.py:34)
   config_environment  .tree_polys, .obstacle_polys, .field_range_poly (check_path_feasibility :423-437)
   search_heuristic    .segment_lanes, .search_lengths, .guided_path, .default_search_length
-Motion type "Pawn" (Dubins goal shots through pydubins) is not supported yet
-and raises NotImplementedError.
+Motion type "Pawn" takes Dubins goal shots (pydubins restated in
+csrc/dubins_core.h, re-splined like get_dubins_path :289-304); "King" takes
+Reeds-Shepp shots.
 """
 import math
 import time
@@ -112,8 +113,6 @@ class HybridAStarSearch(object):
         return (round(x / self.plan_resolution), round(y / self.plan_resolution), round(yaw / self.yaw_resolution))
 
     def lower(self, max_nodes=2000):
-        if self.motion_type != "King":
-            raise NotImplementedError("[HA*] motion_type 'Pawn' (Dubins goal shots) is not supported by the GPU search")
         return lower_problem(self.start_pose, self.goal_pose, self.config_env, self.car_model,
                              self.search_heuristic, self.motion_type, self.yaw_resolution, self.plan_resolution,
                              max_nodes)

@@ -177,7 +177,7 @@ enum {
   HTP_HA_D_FIELD,                      /* field polygon id or -1 */
   HTP_HA_D_GUIDE0, HTP_HA_D_GUIDE1,    /* guide rows [GUIDE0, GUIDE1) */
   HTP_HA_D_MOT0, HTP_HA_D_MOT1,        /* motion rows [MOT0, MOT1) */
-  HTP_HA_D_KING                        /* 1 = King (Reeds-Shepp); Pawn (Dubins) is not supported yet */
+  HTP_HA_D_KING                        /* 1 = King (Reeds-Shepp goal shots), 0 = Pawn (Dubins + spline) */
 };
 enum {
   HTP_HA_FOUND = 0,            /* goal reached (Reeds-Shepp shot or within one cell) */

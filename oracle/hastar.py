@@ -42,6 +42,7 @@ import math
 
 import numpy as np
 
+from . import dubins_spline as ods
 from . import reeds_shepp as ors
 
 # hybrid_a_star_search.py:28-36
@@ -386,6 +387,25 @@ class HybridAStar:
                 return _Node(self.goal.grid, traj, path.cs, c, path.directions, node.grid)
         return None
 
+    def goal_extension_dubins(self, node):
+        """_get_goal_extension_with_dubins_path :184-230 (get_dubins_path :289-304,
+        calculate_dubins_path_cost :162-182; the cost is a (cost, length) tuple there)."""
+        s, g = node.traj[-1], self.goal.traj[-1]
+        res = self.p["res"]
+        smp = ods.dubins_samples([s[0], s[1], s[2]], [g[0], g[1], g[2]], 1.0 / self.curvature, res)
+        pts = np.vstack([np.array(smp), np.array([[g[0], g[1], g[2]]])])
+        xs, ys, yaws, ks, _ = ods.calc_spline_course(pts[:, 0], pts[:, 1], ds=res)
+        path = np.array([xs, ys, yaws, ks]).T
+        cost = node.cost + np.cumsum(np.hypot(np.diff(path[:, 0]), np.diff(path[:, 1])))[-1] * 1
+        cost += angle_wrap(np.max(path[:, -1]) - np.min(path[:, -1])) * 1
+        traj = np.copy(path[:, :3])
+        traj[:, -1] = angle_wrap(traj[:, -1])
+        length = np.cumsum(np.hypot(np.diff(path[:, 0]), np.diff(path[:, 1])))[-1]
+        ks = list(path[:, 3])
+        if not self.collides(traj) and length < MIN_LENGTH_TO_GOAL:
+            return _Node(self.goal.grid, traj, ks, cost, np.ones_like(ks).tolist(), node.grid)
+        return None
+
     def arrival(self, ext, node):
         """check_the_arrival :464-495."""
         goal_node = ext
@@ -405,8 +425,6 @@ class HybridAStar:
     def search(self):
         """hybrid_a_star_search :497-607 -> dict(xs, ys, yaws, dirs, ks, counter, status, expanded)."""
         p = self.p
-        if not p["king"]:
-            raise NotImplementedError("Pawn (Dubins goal extension) is not restated yet")
         self.start = self.init_node(p["start"])
         self.goal = self.init_node(p["goal"])
         open_set = {self.start.grid: self.start}
@@ -433,7 +451,7 @@ class HybridAStar:
                 cur = open_set.pop(idx)
                 closed[idx] = cur
                 expanded.append(idx)
-                ext = self.goal_extension(cur)
+                ext = self.goal_extension(cur) if p["king"] else self.goal_extension_dubins(cur)
                 gn = self.arrival(ext, cur)
                 if gn is not None:
                     closed[gn.grid] = gn

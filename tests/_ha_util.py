@@ -41,6 +41,27 @@ def scenario(seed, n_obs=None, res=0.2, max_nodes=150, return_objects=False):
     return prob
 
 
+def scenario_pawn(seed, max_nodes=60, res=0.2, n_obs=0):
+    """Pawn (Dubins goal shots): the goal sits in the headland, headed along it,
+    so forward Dubins turns can reach it."""
+    from headland_trajectory_planning_amd.path_planner.hybrid_a_star_search import motion_steers
+    rng = np.random.default_rng(500 + seed)
+    np.random.seed(seed)
+    row_w = rng.uniform(2.4, 3.2)
+    rows = map_utils.create_tree_rows(8, row_w, 20.0, slope_angle=math.radians(rng.uniform(-5, 5)), l_std=0.0)
+    s_row = int(rng.integers(0, 3))
+    e_row = s_row + int(rng.integers(2, 4))
+    start = map_utils.get_base_pose(s_row, rows, rng.uniform(0.5, 1.5), pose_type=map_utils.LEAVE_POSE)
+    goal = map_utils.get_base_pose(e_row, rows, rng.uniform(3.5, 4.5), pose_type=map_utils.ENTER_POSE)
+    goal[2] = math.pi / 2 + rng.uniform(-0.2, 0.2)
+    obs = [[(start[0] + goal[0]) / 2 + rng.uniform(-1.5, 1.5), rng.uniform(start[1], goal[1])] for _ in range(n_obs)]
+    env = OrchardGeometryEnvironment(rows, obs, tree_width=0.3, headland_width=rng.uniform(7.0, 9.0))
+    car = CarModel(max_steer=0.55, axle_to_front=3.0, axle_to_back=0.55, width=1.48)
+    wp = env.get_topology_waypoints(start, goal, drive_row_offset=4.5)
+    heur = ReferenceLineHeuristic(wp, goal, car)
+    return lower_problem(start, goal, env, car, heur, "Pawn", math.radians(10), res, max_nodes)
+
+
 def oracle_problem(p):
     return oha.hastar_problem(p["start"], p["goal"], p["body"], p["blockers"], p["field"], p["lanes"],
                               p["search_lengths"], p["guide"], king=p["king"], res=p["res"], yaw_res=p["yaw_res"],

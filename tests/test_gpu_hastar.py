@@ -39,6 +39,17 @@ def test_gpu_matches_host_core_batch(ctx):
     assert len({r["status"] for r in g}) >= 2
 
 
+def test_gpu_pawn_matches_host_and_oracle(ctx):
+    probs = [U.scenario_pawn(s, n_obs=1 + s % 3) for s in range(16)]
+    g = _gpu(ctx, probs)
+    h = H.as_dicts(H.hastar_host(probs))
+    for a, b in zip(h, g):
+        assert U.compare(a, b, exact=False) == []
+    for p, b in list(zip(probs, g))[:6]:
+        assert U.compare(U.run_oracle(p), b, exact=False) == []
+    assert {r["status"] for r in g} >= {0, 2}
+
+
 def test_gpu_edge_cases_and_bad_input(ctx):
     base = U.scenario(0, max_nodes=30)
     probs = [dict(base, max_nodes=0), dict(base, goal=base["start"].copy()), dict(base, field=None)]

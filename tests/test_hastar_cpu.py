@@ -105,3 +105,13 @@ def test_batch_mixed_problems_host():
     for p, h in zip(probs, hb):
         h1 = H.as_dicts(H.hastar_host([p]))[0]
         assert U.compare(h1, h) == []
+
+
+@pytest.mark.parametrize("seed", [0, 2, 3, 7, 8, 9])
+def test_host_core_matches_oracle_pawn(seed):
+    """Pawn: Dubins goal shots re-splined (scipy CubicSpline in the oracle, the
+    kernel's own not-a-knot solve): identical structure, samples within 1e-9."""
+    p = U.scenario_pawn(seed, n_obs=1 + seed % 3)
+    o = U.run_oracle(p)
+    h = H.as_dicts(H.hastar_host([p]))[0]
+    assert U.compare(o, h, exact=False, tol=1e-9) == []
