@@ -83,7 +83,8 @@ EXPORTS = ["htp_obca_sizes", "htp_create", "htp_destroy", "htp_last_error", "htp
            "htp_obca_solve_batch", "htp_obca_solve_batch_device", "htp_last_kernel_ms", "htp_last_cycles",
            "htp_rs_all_paths_batch", "htp_rs_all_paths_batch_device", "htp_rs_last_ms",
            "htp_hastar_search_batch", "htp_hastar_search_batch_device", "htp_hastar_last_ms",
-           "htp_ypark_search_batch", "htp_ypark_search_batch_device", "htp_ypark_last_ms"]
+           "htp_ypark_search_batch", "htp_ypark_search_batch_device", "htp_ypark_last_ms",
+           "htp_obca_points_sizes", "htp_obca_points_solve_batch", "htp_obca_points_solve_batch_device"]
 
 
 def _declare(lib):
@@ -102,6 +103,14 @@ def _declare(lib):
     lib.htp_obca_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ObcaBatch),
                                                 ctypes.POINTER(ObcaResult), ctypes.c_void_p]
     lib.htp_obca_solve_batch_device.restype = ctypes.c_int
+    lib.htp_obca_points_sizes.argtypes = [ctypes.c_int32] * 3 + [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int64)] * 4
+    lib.htp_obca_points_sizes.restype = ctypes.c_int
+    lib.htp_obca_points_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ObcaPointsBatch),
+                                                ctypes.POINTER(ObcaResult)]
+    lib.htp_obca_points_solve_batch.restype = ctypes.c_int
+    lib.htp_obca_points_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ObcaPointsBatch),
+                                                       ctypes.POINTER(ObcaResult), ctypes.c_void_p]
+    lib.htp_obca_points_solve_batch_device.restype = ctypes.c_int
     lib.htp_last_kernel_ms.argtypes = [ctypes.c_void_p]
     lib.htp_last_kernel_ms.restype = ctypes.c_double
     lib.htp_last_cycles.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
@@ -239,6 +248,67 @@ class PackedBatch:
         b.obs_edges, b.body_edges = self.obs_edges.ctypes.data, self.body_edges.ctypes.data
         src = ptrs or {}
         for name in ("traj", "obs_A", "obs_b", "body_G", "body_g", "params", "init_control", "init_mu", "init_lambda"):
+            setattr(b, name, src[name] if name in src else ptr(getattr(self, name)))
+        return b
+
+
+class ObcaPointsBatch(ctypes.Structure):  # htp_obca_points_batch
+    _fields_ = [("batch", ctypes.c_int32), ("N", ctypes.c_int32), ("M", ctypes.c_int32),
+                ("n_vertices", ctypes.c_int32), ("obs_edges", ctypes.c_void_p), ("traj", ctypes.c_void_p),
+                ("obs_A", ctypes.c_void_p), ("obs_b", ctypes.c_void_p), ("vertices", ctypes.c_void_p),
+                ("params", ctypes.c_void_p), ("init_control", ctypes.c_void_p)]
+
+
+def points_params_of(inst):
+    """HTP_P_* slots of a point-formulation instance (oracle/nlp_points.py format)."""
+    p = np.zeros(NPARAM)
+    p[P_DT] = inst["dT"]
+    p[P_WHEELBASE] = inst["wheelbase"]
+    p[P_MAXSTEER] = inst["max_steer"]
+    p[P_MAXV] = inst["max_velocity"]
+    p[P_MAXACC] = inst["max_accel"]
+    p[P_MAXSR] = inst["max_steer_rate"]
+    p[P_DMIN] = inst["min_dist"]
+    xb = inst.get("x_bound", [-9999999, 9999999])
+    yb = inst.get("y_bound", [-9999999, 9999999])
+    p[P_XLO], p[P_XHI], p[P_YLO], p[P_YHI] = xb[0], xb[1], yb[0], yb[1]
+    p[P_HAS_INIT_CONTROL] = inst.get("init_control") is not None
+    return p
+
+
+class PointsPackedBatch:
+    """Contiguous problem-major arrays of a batch of point-formulation problems
+    (R/obca_py/optimizer_points.py); all share N, obstacle edge counts and the
+    number of hull vertices."""
+
+    def __init__(self, insts):
+        i0 = insts[0]
+        self.batch = len(insts)
+        self.N = int(np.asarray(i0["init_traj"]).shape[0])
+        self.M = len(i0["obs_A"])
+        self.n_vertices = int(np.asarray(i0["vertices"]).shape[0])
+        self.obs_edges = np.array([a.shape[0] for a in i0["obs_A"]], dtype=np.int32)
+        for it in insts:
+            if (np.asarray(it["init_traj"]).shape[0] != self.N
+                    or [a.shape[0] for a in it["obs_A"]] != list(self.obs_edges)
+                    or np.asarray(it["vertices"]).shape[0] != self.n_vertices):
+                raise ValueError("[OBCA points] all problems of a batch must share N, edge and vertex counts")
+        self.traj = np.ascontiguousarray(np.stack([np.asarray(it["init_traj"], dtype=np.float64) for it in insts]))
+        self.obs_A = np.ascontiguousarray(np.stack([np.concatenate(it["obs_A"], axis=0) for it in insts]))
+        self.obs_b = np.ascontiguousarray(np.stack([np.concatenate(it["obs_b"]) for it in insts]))
+        self.vertices = np.ascontiguousarray(np.stack([np.asarray(it["vertices"], dtype=np.float64) for it in insts]))
+        self.params = np.ascontiguousarray(np.stack([points_params_of(it) for it in insts]))
+        self.init_control = PackedBatch._opt(insts, "init_control")
+        self.n_var = 5 * self.N + 2 * (self.N - 1) + self.N * int(self.obs_edges.sum())
+
+    def struct(self, ptrs=None):
+        def ptr(a):
+            return None if a is None else a.ctypes.data
+        b = ObcaPointsBatch()
+        b.batch, b.N, b.M, b.n_vertices = self.batch, self.N, self.M, self.n_vertices
+        b.obs_edges = self.obs_edges.ctypes.data
+        src = ptrs or {}
+        for name in ("traj", "obs_A", "obs_b", "vertices", "params", "init_control"):
             setattr(b, name, src[name] if name in src else ptr(getattr(self, name)))
         return b
 
@@ -460,6 +530,15 @@ class Context:
         rc = self.lib.htp_obca_solve_batch(self.ctx, ctypes.byref(b), ctypes.byref(r))
         if rc != 0:
             raise RuntimeError(f"[htp] htp_obca_solve_batch failed: {self.error()}")
+        return res
+
+    def solve_points(self, packed):
+        """Batched optimizer_points.py solve (host buffers)."""
+        res = HostResults(packed.batch, packed.n_var)
+        b, r = packed.struct(), res.struct()
+        rc = self.lib.htp_obca_points_solve_batch(self.ctx, ctypes.byref(b), ctypes.byref(r))
+        if rc != 0:
+            raise RuntimeError(f"[htp] htp_obca_points_solve_batch failed: {self.error()}")
         return res
 
     def solve_device(self, packed, dev_ptrs, out_ptrs, stream=None):

@@ -17,6 +17,7 @@ constexpr int NC = 2;       // control [accel, steer_rate]
 constexpr int MAXM = 16;    // obstacles per problem
 constexpr int MAXK = 4;     // vehicle bodies per problem
 constexpr int MAXE = 8;     // edges per polytope
+constexpr int MAXKV = 16;   // point formulation: vehicle hull vertices
 constexpr int NBMAX = 13;   // stage block: 5 multipliers + 5 x + 2 u + 1 tau
 
 // per-problem scalar parameters (host packs them; see include/htp.h)
@@ -63,6 +64,9 @@ struct Dims {
   int oU, oMU, oLAM, oTAU, oS; // variable offsets (optimizer.py:292-354)
   int eDyn, eTerm, ePair;      // equality-row offsets
   int nb, nw;                  // stage block size (12 + topt), stage w size (7 + topt)
+  int form;                    // 0: optimizer.py, 1: optimizer_points.py (point formulation)
+  int KV;                      // point formulation: vehicle hull vertices (rows per block = 2 KV)
+  int nblk;                    // blocks of the stage chain (N, or N + 1 with a hard terminal block)
 };
 
 // Offsets (in doubles) of the per-problem workspace arrays.
@@ -115,6 +119,33 @@ HTP_HD inline void make_dims(Dims& d, int N, int M, int K, int topt, const int* 
   d.md = 2 * d.P;
   d.nw = 7 + d.topt;
   d.nb = NS + d.nw;
+  d.form = 0;
+  d.KV = 0;
+  d.nblk = N;
+}
+
+// Point formulation (R/obca_py/optimizer_points.py): X (5N), U (2(N-1)), LAMBDA
+// obstacle-major (N * sum_{j'<j} e_j' + i * e_j, :223-255); no mu, tau or terminal
+// slack; equality rows X0, dynamics, X_{N-1} = end (hard, :264-278); per block
+// (obstacle j, step i) 2 KV inequality rows [||A'lam||^2, (A(R v_k + t) - b).lam]
+// for each hull vertex k (:282-327).  The vertices travel in the body_G slot
+// (eb[0] = KV); the stage chain gets one extra block for the terminal rows.
+HTP_HD inline void make_dims_points(Dims& d, int N, int M, int KV, const int* eo) {
+  const int kv[1] = {KV};
+  make_dims(d, N, M, 1, 0, eo, kv);
+  d.form = 1;
+  d.KV = KV;
+  d.mu_count = 0;
+  d.lam_count = d.TEo;
+  d.P = N * M;
+  d.oMU = d.oU + NC * (N - 1);
+  d.oLAM = d.oMU;
+  d.oTAU = d.oLAM + N * d.TEo;
+  d.oS = d.oTAU;
+  d.n = d.oS;
+  d.mc = d.ePair;
+  d.md = 2 * KV * d.P;
+  d.nblk = N + 1;
 }
 
 inline Layout make_layout(const Dims& d) {
@@ -132,8 +163,8 @@ inline Layout make_layout(const Dims& d) {
   L.ct = take(d.mc); L.csoc = take(d.mc); L.syc = take(d.mc);
   L.pairS = take(6 * (int64_t)d.P); L.pairR = take(3 * (int64_t)d.P);
   const int64_t nb2 = (int64_t)d.nb * d.nb;
-  L.Kst = take(d.N * nb2); L.Off = take(d.N * nb2); L.LD = take(d.N * nb2); L.fac = take(d.N * nb2);
-  L.V = take((int64_t)d.N * d.nb); L.X = take((int64_t)d.N * d.nb); L.ipiv = take((int64_t)d.N * d.nb);
+  L.Kst = take(d.nblk * nb2); L.Off = take(d.nblk * nb2); L.LD = take(d.nblk * nb2); L.fac = take(d.nblk * nb2);
+  L.V = take((int64_t)d.nblk * d.nb); L.X = take((int64_t)d.nblk * d.nb); L.ipiv = take((int64_t)d.nblk * d.nb);
   L.total = o;
   return L;
 }

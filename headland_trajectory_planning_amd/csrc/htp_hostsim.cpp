@@ -69,3 +69,36 @@ extern "C" double htp_hostsim_debug_ws(const htp_obca_batch* in, int mode, doubl
   for (int64_t q = 0; q < ws_len && q < L.total; ++q) ws_out[q] = ws[q];
   return S.sf;
 }
+
+// point formulation (optimizer_points.py), serial host build
+extern "C" int htp_hostsim_obca_points_solve(const htp_obca_points_batch* in, htp_obca_result* out,
+                                             const char** names, const double* values, int nopt) {
+  const char* e = nullptr;
+  if (check_shape_points(in, &e)) return -1;
+  Options o = default_options();
+  for (int k = 0; k < nopt; ++k)
+    if (set_option(o, names[k], values[k])) return -2;
+  Dims D;
+  make_dims_points(D, in->N, in->M, in->n_vertices, in->obs_edges);
+  Layout L = make_layout(D);
+  std::vector<double> ws((size_t)L.total);
+  std::vector<double> lds(4 * NBMAX * NBMAX + 8 + 128);
+  std::vector<int> ilds(2 * NBMAX);
+  BatchView b = points_view(in);
+  for (int p = 0; p < in->batch; ++p) {
+    HostLane c;
+    c.lds = lds.data();
+    c.ildsp = ilds.data();
+    ProblemIn pin = problem_view(b, D, p);
+    ObcaSolver<HostLane, 1, MAXE, 1> S(c, D, L, o, pin, ws.data());
+    Result r{};
+    S.run(r);
+    for (int q = 0; q < D.n; ++q) out->x[(size_t)p * D.n + q] = ws[L.x + q];
+    if (out->objective) out->objective[p] = r.objective;
+    if (out->status) out->status[p] = r.status;
+    if (out->iterations) out->iterations[p] = r.iters;
+    if (out->n_factor) out->n_factor[p] = r.n_factor;
+    if (out->nlp_error) out->nlp_error[p] = r.nlp_error;
+  }
+  return 0;
+}

@@ -50,6 +50,32 @@ __global__ __launch_bounds__(64, HTP_WAVES_PER_EU) void obca_solve_kernel(const 
   for (int q = threadIdx.x; q < n; q += 64) xout[(int64_t)p * n + q] = x[q];
 }
 
+// point formulation (optimizer_points.py): the same IPM, lambda-only local blocks
+template <int EM>
+__global__ __launch_bounds__(64, HTP_WAVES_PER_EU) void obca_points_kernel(const Shape* __restrict__ shp, BatchView b,
+                                                                          double* __restrict__ ws_all,
+                                                                          int64_t ws_stride, Result* __restrict__ res,
+                                                                          double* __restrict__ xout, int batch) {
+  __shared__ double lds_[LDS_D];
+  __shared__ int ilds_[2 * NBMAX];
+  DevWave::ld* lds = (DevWave::ld*)lds_;
+  DevWave::li* ilds = (DevWave::li*)ilds_;
+  const int p = blockIdx.x;
+  if (p >= batch) return;
+  DevWave c{(int)threadIdx.x, lds, ilds};
+  using CS = DevWave::cst<Shape>;
+  CS* sh = (CS*)shp;
+  ProblemIn in = problem_view(b, sh->D, p);
+  double* ws = ws_all + (int64_t)p * ws_stride;
+  ObcaSolver<DevWave, 1, EM, 1> S(c, sh->D, sh->L, sh->o, in, ws);
+  Result r{};
+  S.run(r);
+  if (threadIdx.x == 0) res[p] = r;
+  const double* x = ws + sh->L.x;
+  const int n = sh->D.n;
+  for (int q = threadIdx.x; q < n; q += 64) xout[(int64_t)p * n + q] = x[q];
+}
+
 __global__ void unpack_results(const Result* __restrict__ r, int batch, double* obj, int32_t* st, int32_t* it,
                                int32_t* nf, double* err) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -238,6 +264,111 @@ int htp_obca_solve_batch(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result
     struct { void* dst; size_t off, sz; } outs[6] = {{out->x, off[9], sz_x}, {out->objective, off[10], bytes(B)},
                                                      {out->status, off[11], (size_t)B * 4}, {out->iterations, off[12], (size_t)B * 4},
                                                      {out->n_factor, off[13], (size_t)B * 4}, {out->nlp_error, off[14], bytes(B)}};
+    for (auto& o : outs)
+      if (o.dst && hipMemcpy(o.dst, dev + o.off, o.sz, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(ctx, "copy back");
+  }
+  (void)hipFree(dev);
+  return rc;
+}
+
+int htp_obca_points_sizes(int32_t N, int32_t M, int32_t n_vertices, const int32_t* eo, int64_t* n_var,
+                          int64_t* n_eq, int64_t* n_ineq, int64_t* ws_doubles) {
+  if (N < 2 || M < 1 || M > MAXM || n_vertices < 3 || n_vertices > MAXKV || !eo) return -1;
+  Dims D;
+  make_dims_points(D, N, M, n_vertices, eo);
+  Layout L = make_layout(D);
+  if (n_var) *n_var = D.n;
+  if (n_eq) *n_eq = D.mc;
+  if (n_ineq) *n_ineq = D.md;
+  if (ws_doubles) *ws_doubles = L.total;
+  return 0;
+}
+
+int htp_obca_points_solve_batch_device(htp_ctx* ctx, const htp_obca_points_batch* in, htp_obca_result* out,
+                                       void* stream) {
+  if (!ctx || !in || !out) return -1;
+  const char* e = nullptr;
+  if (check_shape_points(in, &e)) return fail(ctx, e);
+  if (in->batch == 0) return 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  Dims D;
+  make_dims_points(D, in->N, in->M, in->n_vertices, in->obs_edges);
+  Layout L = make_layout(D);
+  if (ensure(ctx, &ctx->ws, &ctx->ws_bytes, (size_t)L.total * sizeof(double) * (size_t)in->batch)) return -1;
+  if (ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, sizeof(Result) * (size_t)in->batch)) return -1;
+  if (!ctx->shape) HIPCHK(hipMalloc((void**)&ctx->shape, sizeof(Shape)));
+  Shape hs{D, L, ctx->opt};
+  const BatchView b = points_view(in);
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipMemcpyAsync(ctx->shape, &hs, sizeof(Shape), hipMemcpyHostToDevice, s));
+  HIPCHK(hipEventRecord(ctx->ev0, s));
+  bool u4 = true;
+  for (int m = 0; m < D.M; ++m) u4 = u4 && D.eo[m] == 4;
+  if (u4)
+    hipLaunchKernelGGL((obca_points_kernel<4>), dim3(in->batch), dim3(64), 0, s, (const Shape*)ctx->shape, b,
+                       (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
+  else
+    hipLaunchKernelGGL((obca_points_kernel<MAXE>), dim3(in->batch), dim3(64), 0, s, (const Shape*)ctx->shape, b,
+                       (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ctx->ev1, s));
+  hipLaunchKernelGGL(unpack_results, dim3((in->batch + 255) / 256), dim3(256), 0, s, (const Result*)ctx->scratch,
+                     in->batch, out->objective, out->status, out->iterations, out->n_factor, out->nlp_error);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int htp_obca_points_solve_batch(htp_ctx* ctx, const htp_obca_points_batch* in, htp_obca_result* out) {
+  if (!ctx || !in || !out) return -1;
+  const char* e = nullptr;
+  if (check_shape_points(in, &e)) return fail(ctx, e);
+  if (in->batch == 0) return 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  Dims D;
+  make_dims_points(D, in->N, in->M, in->n_vertices, in->obs_edges);
+  const int64_t B = in->batch;
+  auto bytes = [&](int64_t n) { return (size_t)(n * (int64_t)sizeof(double)); };
+  const size_t sz_in[6] = {bytes(B * D.N * NS), bytes(B * D.TEo * 2), bytes(B * D.TEo), bytes(B * D.KV * 2),
+                           bytes(B * NPARAM), in->init_control ? bytes(B * (D.N - 1) * NC) : 0};
+  const void* srcs[6] = {in->traj, in->obs_A, in->obs_b, in->vertices, in->params, in->init_control};
+  const size_t sz_x = bytes(B * D.n);
+  std::vector<size_t> sizes(sz_in, sz_in + 6);
+  for (size_t v : {sz_x, bytes(B), (size_t)B * 4, (size_t)B * 4, (size_t)B * 4, bytes(B)}) sizes.push_back(v);
+  size_t total = 0;
+  std::vector<size_t> off;
+  for (size_t v : sizes) { off.push_back(total); total += (v + 255) & ~size_t(255); }
+  char* dev = nullptr;
+  HIPCHK(hipMalloc((void**)&dev, total));
+  for (int k = 0; k < 6; ++k)
+    if (sizes[k]) {
+      hipError_t er = hipMemcpy(dev + off[k], srcs[k], sizes[k], hipMemcpyHostToDevice);
+      if (er != hipSuccess) { (void)hipFree(dev); return fail(ctx, hipGetErrorString(er)); }
+    }
+  htp_obca_points_batch din = *in;
+  din.traj = (const double*)(dev + off[0]);
+  din.obs_A = (const double*)(dev + off[1]);
+  din.obs_b = (const double*)(dev + off[2]);
+  din.vertices = (const double*)(dev + off[3]);
+  din.params = (const double*)(dev + off[4]);
+  din.init_control = sizes[5] ? (const double*)(dev + off[5]) : nullptr;
+  htp_obca_result dout;
+  dout.x = (double*)(dev + off[6]);
+  dout.objective = (double*)(dev + off[7]);
+  dout.status = (int32_t*)(dev + off[8]);
+  dout.iterations = (int32_t*)(dev + off[9]);
+  dout.n_factor = (int32_t*)(dev + off[10]);
+  dout.nlp_error = (double*)(dev + off[11]);
+  int rc = htp_obca_points_solve_batch_device(ctx, &din, &dout, nullptr);
+  if (rc == 0) {
+    hipError_t er = hipDeviceSynchronize();
+    if (er != hipSuccess) rc = fail(ctx, std::string("points solve kernel: ") + hipGetErrorString(er));
+  }
+  if (rc == 0) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) == hipSuccess) ctx->last_ms = ms;
+    struct { void* dst; size_t off, sz; } outs[6] = {{out->x, off[6], sz_x}, {out->objective, off[7], bytes(B)},
+                                                     {out->status, off[8], (size_t)B * 4}, {out->iterations, off[9], (size_t)B * 4},
+                                                     {out->n_factor, off[10], (size_t)B * 4}, {out->nlp_error, off[11], bytes(B)}};
     for (auto& o : outs)
       if (o.dst && hipMemcpy(o.dst, dev + o.off, o.sz, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(ctx, "copy back");
   }

@@ -40,6 +40,22 @@ inline int check_shape(const htp_obca_batch* in, const char** err) {
   return 0;
 }
 
+inline int check_shape_points(const htp_obca_points_batch* in, const char** err) {
+  if (in->batch < 0) { *err = "[OBCA points] batch must be >= 0"; return -1; }
+  if (in->N < 2) { *err = "[OBCA points] N must be >= 2"; return -1; }
+  if (in->M < 1 || in->M > MAXM) { *err = "[OBCA points] M must be in [1, 16]"; return -1; }
+  if (in->n_vertices < 3 || in->n_vertices > MAXKV) { *err = "[OBCA points] n_vertices must be in [3, 16]"; return -1; }
+  for (int m = 0; m < in->M; ++m)
+    if (in->obs_edges[m] < 3 || in->obs_edges[m] > MAXE) { *err = "[OBCA points] obstacle edges must be in [3, 8]"; return -1; }
+  return 0;
+}
+
+// point formulation: vertices ride in the body_G slot (Dims::eb[0] = KV)
+inline BatchView points_view(const htp_obca_points_batch* in) {
+  return BatchView{in->traj, in->obs_A, in->obs_b, in->vertices, in->vertices, in->params,
+                   in->init_control, nullptr, nullptr};
+}
+
 inline int set_option(Options& o, const char* name, double v) {
 #define HTP_OPT(f) if (!std::strcmp(name, #f)) { o.f = (decltype(o.f))v; return 0; }
   HTP_OPT(tol) HTP_OPT(dual_inf_tol) HTP_OPT(constr_viol_tol) HTP_OPT(compl_inf_tol)

@@ -111,6 +111,55 @@ struct LocalBlock {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Point-formulation local block (R/obca_py/optimizer_points.py:282-327):
+// z = lam_ji (EM) of obstacle j at step i, no equality rows; its 2 KV
+// inequality rows (||A'lam||^2 in [0,1], (A(R v_k + t) - b).lam in
+// [dmin, 1e5] for every hull vertex k) are eliminated, leaving
+// Hbar_zz (+ coupling to p = (x, y, theta)).  IPOPT's inertia needs Hbar_zz
+// positive definite: a non-positive pivot sets `piv` and the exact counts
+// come from the Bunch-Kaufman path.
+// ---------------------------------------------------------------------------
+template <int EM>
+struct PtBlock {
+  static constexpr int NZ = EM;
+  static constexpr int NL = EM;
+  static constexpr int NPK = NZ * (NZ + 1) / 2;
+  double K[NPK];
+  double B[NZ][3];
+  double Hpp[6];
+  int neg, zero;
+  bool piv;
+
+  HTP_HD HTP_FI static int pk(int r, int c) { return r * (r + 1) / 2 + c; }
+  HTP_HD HTP_FI void factor() {
+    neg = 0;
+    zero = 0;
+    piv = false;
+    for (int k = 0; k < NL; ++k) {
+      double dk = K[pk(k, k)];
+      for (int j = 0; j < k; ++j) dk -= K[pk(k, j)] * K[pk(k, j)] * K[pk(j, j)];
+      for (int r = k + 1; r < NL; ++r) {
+        double v = K[pk(r, k)];
+        for (int j = 0; j < k; ++j) v -= K[pk(r, j)] * K[pk(k, j)] * K[pk(j, j)];
+        K[pk(r, k)] = v;
+      }
+      if (!(dk > 0.0)) piv = true;
+      if (dk == 0.0) { zero = 1; dk = 1.0; }
+      if (dk < 0.0) ++neg;
+      K[pk(k, k)] = dk;
+      for (int r = k + 1; r < NL; ++r) K[pk(r, k)] = K[pk(r, k)] / dk;
+    }
+  }
+  HTP_HD HTP_FI void solve(double* v) const {
+    for (int k = 0; k < NL; ++k)
+      for (int j = 0; j < k; ++j) v[k] -= K[pk(k, j)] * v[j];
+    for (int k = 0; k < NL; ++k) v[k] /= K[pk(k, k)];
+    for (int k = NL - 1; k >= 0; --k)
+      for (int r = k + 1; r < NL; ++r) v[k] -= K[pk(r, k)] * v[r];
+  }
+};
+
 // Bunch-Kaufman LDL^T (LAPACK dsytf2 / dsytrs, lower) of a packed symmetric
 // n x n matrix, for the rare local blocks that need interchanges.  Run-time
 // indexing: these live in their own (not inlined) frame.
@@ -216,8 +265,9 @@ HTP_HD inline void bk_solve_packed(const double* K, const int* ip, int n, double
 }
 
 // ---------------------------------------------------------------------------
-template <class Ctx, int EN_ = 4, int EM_ = 4>
+template <class Ctx, int EN_ = 4, int EM_ = 4, int FORM_ = 0>
 struct ObcaSolver {
+  static constexpr bool PT = FORM_ == 1;  // point formulation (optimizer_points.py)
   using gd = typename Ctx::gd;  // workspace / input arrays (HBM)
   using ld = typename Ctx::ld;  // per-wave LDS scratch
   using li = typename Ctx::li;
@@ -257,6 +307,14 @@ struct ObcaSolver {
 
   // pair p -> (i, m, n) and variable offsets
   HTP_HD HTP_FI void pair_index(int p, int& i, int& m, int& n, int& mu0, int& la0) const {
+    if constexpr (PT) {  // block p = (obstacle m, step i), obstacle-major
+      m = p / D.N;
+      i = p - m * D.N;
+      n = 0;
+      la0 = D.oLAM + D.N * D.offo[m] + i * D.eo[m];
+      mu0 = la0;
+      return;
+    }
     n = p % D.K;
     int t = p / D.K;
     m = t % D.M;
@@ -264,6 +322,10 @@ struct ObcaSolver {
     mu0 = D.oMU + i * D.mu_count + m * D.TEb + D.offb[n];
     la0 = D.oLAM + i * D.lam_count + n * D.TEo + D.offo[m];
   }
+
+  // local block q of stage i, and the number of local blocks per stage
+  HTP_HD HTP_FI int blk(int i, int q) const { return PT ? q * D.N + i : i * (D.M * D.K) + q; }
+  HTP_HD HTP_FI int blocks_per_stage() const { return PT ? D.M : D.M * D.K; }
 
   // stage w = [x_i (5), u_i (2), tau_i]
   HTP_HD HTP_FI void stage_w(const gd* x, int i, double* w) const {
@@ -291,6 +353,17 @@ struct ObcaSolver {
     const int N = D.N;
     const double dT = par(P_DT);
     double f = 0.0;
+    if constexpr (PT) {  // optimizer_points.py generate_object :193-227
+      if (i < N - 1) {
+        if (i < N - 2) {
+          const double dsr = x[D.oU + NC * (i + 1) + 1] - x[D.oU + NC * i + 1];
+          const double dv = x[D.oU + NC * (i + 1)] - x[D.oU + NC * i];
+          f += dsr * dsr + dv * dv;
+        }
+        f += sq(x[NS * i + 2] * dT) * 20.0;
+      }
+      return f;
+    }
     if (i < N - 1) {
       const double h = dT * tauv(x, i);
       const double a = x[D.oU + NC * i], w = x[D.oU + NC * i + 1];
@@ -320,6 +393,25 @@ struct ObcaSolver {
     HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) g[q] = 0.0;
     c.sync();
+    if constexpr (PT) {
+      for (int i = c.lane; i < N - 1; i += c.width) {
+        const double a = x[D.oU + NC * i], w = x[D.oU + NC * i + 1];
+        double ga = 0.0, gw = 0.0;
+        if (i < N - 2) {
+          ga -= 2.0 * (x[D.oU + NC * (i + 1)] - a);
+          gw -= 2.0 * (x[D.oU + NC * (i + 1) + 1] - w);
+        }
+        if (i >= 1) {
+          ga += 2.0 * (a - x[D.oU + NC * (i - 1)]);
+          gw += 2.0 * (w - x[D.oU + NC * (i - 1) + 1]);
+        }
+        g[NS * i + 2] = scale * (40.0 * x[NS * i + 2] * dT * dT);
+        g[D.oU + NC * i] = scale * ga;
+        g[D.oU + NC * i + 1] = scale * gw;
+      }
+      c.sync();
+      return;
+    }
     for (int i = c.lane; i < N - 1; i += c.width) {
       const double tau = tauv(x, i), h = dT * tau;
       const double a = x[D.oU + NC * i], w = x[D.oU + NC * i + 1];
@@ -367,6 +459,47 @@ struct ObcaSolver {
     sn = sin(th);
   }
 
+  // point formulation: obstacle halfspaces, lam, w = A'lam and the pose of block p
+  struct PtGeom {
+    double A0[EM_], A1[EM_], bb[EM_], lam[EM_];
+    double w0, w1, cs, sn, tx, ty;
+    int i, m, em, la0;
+  };
+  HTP_HD HTP_FI void pt_geom(const gd* x, int p, PtGeom& G) const {
+    int n_, mu0_;
+    pair_index(p, G.i, G.m, n_, mu0_, G.la0);
+    G.em = D.eo[G.m];
+    const gd* Am = gp(in.obsA) + 2 * D.offo[G.m];
+    const gd* bm = gp(in.obsb) + D.offo[G.m];
+    G.w0 = 0.0;
+    G.w1 = 0.0;
+    for (int j = 0; j < EM_; ++j) {
+      const bool on = j < G.em;
+      G.A0[j] = on ? Am[2 * j] : 0.0;
+      G.A1[j] = on ? Am[2 * j + 1] : 0.0;
+      G.bb[j] = on ? bm[j] : 0.0;
+      G.lam[j] = on ? x[G.la0 + j] : 0.0;
+      G.w0 += G.A0[j] * G.lam[j];
+      G.w1 += G.A1[j] * G.lam[j];
+    }
+    const double th = x[NS * G.i + 3];
+    G.cs = cos(th);
+    G.sn = sin(th);
+    G.tx = x[NS * G.i];
+    G.ty = x[NS * G.i + 1];
+  }
+  // hull vertex k of the body frame: moved vertex vt = R v + t, dR/dth v, R v
+  HTP_HD HTP_FI void pt_vertex(const PtGeom& G, int k, double* vt, double* dv, double* rv) const {
+    const gd* V = gp(in.bodyG);
+    const double v0 = V[2 * k], v1 = V[2 * k + 1];
+    rv[0] = G.cs * v0 - G.sn * v1;
+    rv[1] = G.sn * v0 + G.cs * v1;
+    vt[0] = rv[0] + G.tx;
+    vt[1] = rv[1] + G.ty;
+    dv[0] = -G.sn * v0 - G.cs * v1;
+    dv[1] = G.cs * v0 - G.sn * v1;
+  }
+
   HTP_HD HTP_FI void pair_cons(const gd* x, int p, double* out4) const {
     double w[2], cs, sn;
     int i, m, n, mu0, la0;
@@ -409,9 +542,28 @@ struct ObcaSolver {
       } else {
         for (int k = 0; k < NS; ++k) {
           const int r = D.eTerm + k;
-          cc[r] = scE[r] * (x[NS * i + k] - gp(in.traj)[NS * i + k] + x[D.oS + k]);
+          if constexpr (PT) cc[r] = scE[r] * (x[NS * i + k] - gp(in.traj)[NS * i + k]);
+          else cc[r] = scE[r] * (x[NS * i + k] - gp(in.traj)[NS * i + k] + x[D.oS + k]);
         }
       }
+    }
+    if constexpr (PT) {
+      const int KV = D.KV;
+      for (int p = c.lane; p < D.P; p += c.width) {
+        PtGeom G;
+        pt_geom(x, p, G);
+        for (int k = 0; k < KV; ++k) {
+          double vt[2], dv[2], rv[2];
+          pt_vertex(G, k, vt, dv, rv);
+          double dist = 0.0;
+          for (int j = 0; j < EM_; ++j) dist += (G.A0[j] * vt[0] + G.A1[j] * vt[1] - G.bb[j]) * G.lam[j];
+          const int r = 2 * (KV * p + k);
+          dd[r] = scI[r] * (G.w0 * G.w0 + G.w1 * G.w1);
+          dd[r + 1] = scI[r + 1] * dist;
+        }
+      }
+      c.sync();
+      return;
     }
     for (int p = c.lane; p < D.P; p += c.width) {
       double v[4];
@@ -434,6 +586,32 @@ struct ObcaSolver {
     HTP_UNROLL
     for (int q = c.lane; q < D.n; q += c.width) out[q] = 0.0;
     c.sync();
+    if constexpr (PT) {
+      const int KV = D.KV;
+      for (int p = c.lane; p < D.P; p += c.width) {
+        PtGeom G;
+        pt_geom(x, p, G);
+        double ol[EM_];
+        for (int j = 0; j < EM_; ++j) ol[j] = 0.0;
+        double px = 0.0, py = 0.0, pt = 0.0;
+        for (int k = 0; k < KV; ++k) {
+          const int r = 2 * (KV * p + k);
+          const double y1 = scI[r] * yd[r], y3 = scI[r + 1] * yd[r + 1];
+          double vt[2], dv[2], rv[2];
+          pt_vertex(G, k, vt, dv, rv);
+          for (int j = 0; j < EM_; ++j)
+            ol[j] += 2.0 * (G.A0[j] * G.w0 + G.A1[j] * G.w1) * y1 + (G.A0[j] * vt[0] + G.A1[j] * vt[1] - G.bb[j]) * y3;
+          px += G.w0 * y3;
+          py += G.w1 * y3;
+          pt += (G.w0 * dv[0] + G.w1 * dv[1]) * y3;
+        }
+        for (int j = 0; j < EM_; ++j)
+          if (j < G.em) out[G.la0 + j] = ol[j];
+        pr[3 * p + 0] = px;
+        pr[3 * p + 1] = py;
+        pr[3 * p + 2] = pt;
+      }
+    } else
     for (int p = c.lane; p < D.P; p += c.width) {
       double w[2], cs, sn;
       int i, m, n, mu0, la0;
@@ -458,7 +636,7 @@ struct ObcaSolver {
       pr[3 * p + 2] = (-sn * w[0] + cs * w[1]) * ya + (-cs * w[0] - sn * w[1]) * yb;
     }
     c.sync();
-    const int MK = D.M * D.K;
+    const int MK = blocks_per_stage();
     for (int i = c.lane; i < N; i += c.width) {
       double gx[5] = {0, 0, 0, 0, 0};
       if (i == 0)
@@ -469,7 +647,7 @@ struct ObcaSolver {
         for (int k = 0; k < NS; ++k) {
           const double t = scE[D.eTerm + k] * yc[D.eTerm + k];
           gx[k] += t;
-          out[D.oS + k] = t;
+          if constexpr (!PT) out[D.oS + k] = t;
         }
       } else {
         double w[8], J[40], yy[5];
@@ -485,7 +663,7 @@ struct ObcaSolver {
         if (D.topt) out[D.oTAU + i] = gw[7];
       }
       for (int q = 0; q < MK; ++q) {
-        const int p = i * MK + q;
+        const int p = blk(i, q);
         gx[0] += pr[3 * p];
         gx[1] += pr[3 * p + 1];
         gx[3] += pr[3 * p + 2];
@@ -524,8 +702,14 @@ struct ObcaSolver {
         v0 = in.init_mu ? gp(in.init_mu)[q - D.oMU] : 0.1;
         lo = 0.0;
       } else if (q < D.oTAU) {
-        v0 = in.init_la ? gp(in.init_la)[q - D.oLAM] : 0.1;
-        lo = 0.0;
+        if constexpr (PT) {  // optimizer_points.py:101-104 (init_dual_var unused), :252-255
+          v0 = 0.1;
+          lo = 0.0;
+          hi = 100000.0;
+        } else {
+          v0 = in.init_la ? gp(in.init_la)[q - D.oLAM] : 0.1;
+          lo = 0.0;
+        }
       } else if (q < D.oS) {
         v0 = 1.0;
         lo = 0.05 / par(P_DT);
@@ -569,6 +753,27 @@ struct ObcaSolver {
       } else {
         for (int k = 0; k < NS; ++k) scE[D.eTerm + k] = 1.0;
       }
+    }
+    if constexpr (PT) {
+      const int KV = D.KV;
+      for (int p = c.lane; p < D.P; p += c.width) {
+        PtGeom G;
+        pt_geom(x, p, G);
+        double r1 = 0.0;
+        for (int j = 0; j < EM_; ++j) r1 = dmax(r1, dabs(2.0 * (G.A0[j] * G.w0 + G.A1[j] * G.w1)));
+        for (int k = 0; k < KV; ++k) {
+          double vt[2], dv[2], rv[2];
+          pt_vertex(G, k, vt, dv, rv);
+          double r3 = dmax(dabs(G.w0), dabs(G.w1));
+          r3 = dmax(r3, dabs(G.w0 * dv[0] + G.w1 * dv[1]));
+          for (int j = 0; j < EM_; ++j) r3 = dmax(r3, dabs(G.A0[j] * vt[0] + G.A1[j] * vt[1] - G.bb[j]));
+          const int r = 2 * (KV * p + k);
+          scI[r] = scl(r1);
+          scI[r + 1] = scl(r3);
+        }
+      }
+      c.sync();
+      return;
     }
     for (int p = c.lane; p < D.P; p += c.width) {
       double w[2], cs, sn;
@@ -646,7 +851,7 @@ struct ObcaSolver {
     HTP_UNROLL
     for (int r = c.lane; r < D.md; r += c.width) {
       double lo, hi;
-      if ((r & 1) == 0) { lo = 0.0; hi = 1.0; } else { lo = dmn; hi = HTP_INF; }
+      if ((r & 1) == 0) { lo = 0.0; hi = 1.0; } else { lo = dmn; hi = PT ? 100000.0 : HTP_INF; }
       const bool hl = true, hu = finite_(hi);
       lo -= rf * dmax(1.0, dabs(lo));
       if (hu) hi += rf * dmax(1.0, dabs(hi));
@@ -812,6 +1017,10 @@ struct ObcaSolver {
 
   template <int EN, int EM>
   HTP_HD HTP_FI void local_factor_sweep(bool ls, double dw, double dc, int& neg, int& zero) {
+    if constexpr (PT) {
+      local_factor_sweep_pt(ls, dw, dc, neg, zero);
+      return;
+    }
     gd* PS = A(L.pairS);
     for (int p = c.lane; p < D.P; p += c.width) {
       LocalBlock<EN, EM> B;
@@ -853,6 +1062,10 @@ struct ObcaSolver {
   template <int EN, int EM>
   HTP_HD HTP_FI void local_rhs_sweep(bool ls, double dw, double dc, const gd* bx, const gd* bs,
                               const gd* bc, const gd* bd) {
+    if constexpr (PT) {
+      local_rhs_sweep_pt(ls, dw, dc, bx, bs, bd);
+      return;
+    }
     gd* PR = A(L.pairR);
     for (int p = c.lane; p < D.P; p += c.width) {
       LocalBlock<EN, EM> B;
@@ -892,6 +1105,10 @@ struct ObcaSolver {
   HTP_HD HTP_FI void local_back_sweep(bool ls, double dw, double dc, const gd* bx, const gd* bs,
                                const gd* bc, const gd* bd, gd* ox, gd* os, gd* oc,
                                gd* od) {
+    if constexpr (PT) {
+      local_back_sweep_pt(ls, dw, dc, bx, bs, bd, ox, os, od);
+      return;
+    }
     for (int p = c.lane; p < D.P; p += c.width) {
       LocalBlock<EN, EM> B;
       build_local<EN, EM>(B, p, ls, dw, dc);
@@ -935,6 +1152,243 @@ struct ObcaSolver {
       od[2 * p + 1] = y3;
       os[2 * p] = (bs[2 * p] + y1) / B.Ds1;
       os[2 * p + 1] = (bs[2 * p + 1] + y3) / B.Ds3;
+    }
+  }
+
+  // ---------------------------------------------------- point-formulation blocks
+  // eliminated inequality rows of block p, vertex k: diagonal Ds and E = 1/Ds + dc
+  HTP_HD HTP_FI void pt_row_e(int p, int k, bool ls, double dw, double dc, double& Ds1, double& E1, double& Ds3,
+                              double& E3) const {
+    const int r1 = 2 * (D.KV * p + k), r3 = r1 + 1;
+    if (ls) {
+      Ds1 = 1.0;
+      Ds3 = 1.0;
+    } else {
+      const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
+      const gd* vL = A(L.vL); const gd* vU = A(L.vU);
+      Ds1 = vL[r1] / (s[r1] - dL[r1]) + vU[r1] / (dU[r1] - s[r1]) + dw;
+      Ds3 = vL[r3] / (s[r3] - dL[r3]) + vU[r3] / (dU[r3] - s[r3]) + dw;
+    }
+    E1 = 1.0 / Ds1 + dc;
+    E3 = 1.0 / Ds3 + dc;
+  }
+  // scaled Jacobian rows of block p, vertex k: J1 = s1 2 A w (z only), J3 = [J3z | J3p]
+  HTP_HD HTP_FI void pt_row_jac(const PtGeom& G, int p, int k, double& s1, double* J3z, double* J3p, double* dv,
+                                double* rv) const {
+    const gd* scI = A(L.scI);
+    const int r1 = 2 * (D.KV * p + k);
+    s1 = scI[r1];
+    const double s3 = scI[r1 + 1];
+    double vt[2];
+    pt_vertex(G, k, vt, dv, rv);
+    for (int j = 0; j < EM_; ++j) J3z[j] = s3 * (G.A0[j] * vt[0] + G.A1[j] * vt[1] - G.bb[j]);
+    J3p[0] = s3 * G.w0;
+    J3p[1] = s3 * G.w1;
+    J3p[2] = s3 * (G.w0 * dv[0] + G.w1 * dv[1]);
+  }
+
+  HTP_HD HTP_FI void build_local_pt(PtBlock<EM_>& B, const PtGeom& G, int p, bool ls, double dw, double dc) const {
+    const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
+    const gd* zL = A(L.zL); const gd* zU = A(L.zU);
+    const gd* scI = A(L.scI); const gd* yd = A(L.yd);
+    constexpr int NZ = EM_;
+    for (int q = 0; q < PtBlock<EM_>::NPK; ++q) B.K[q] = 0.0;
+    for (int r = 0; r < NZ; ++r) B.B[r][0] = B.B[r][1] = B.B[r][2] = 0.0;
+    for (int q = 0; q < 6; ++q) B.Hpp[q] = 0.0;
+    double Aw2[EM_];
+    for (int j = 0; j < EM_; ++j) Aw2[j] = 2.0 * (G.A0[j] * G.w0 + G.A1[j] * G.w1);
+    double y1sum = 0.0;
+    for (int k = 0; k < D.KV; ++k) {
+      double Ds1, E1, Ds3, E3, s1, J3z[EM_], J3p[3], dv[2], rv[2];
+      pt_row_e(p, k, ls, dw, dc, Ds1, E1, Ds3, E3);
+      pt_row_jac(G, p, k, s1, J3z, J3p, dv, rv);
+      const double iE3 = 1.0 / E3, c1 = s1 * s1 / E1;
+      for (int r = 0; r < NZ; ++r)
+        for (int q = 0; q <= r; ++q) B.K[B.pk(r, q)] += c1 * Aw2[r] * Aw2[q] + J3z[r] * J3z[q] * iE3;
+      for (int r = 0; r < NZ; ++r)
+        for (int col = 0; col < 3; ++col) B.B[r][col] += J3z[r] * J3p[col] * iE3;
+      B.Hpp[0] += J3p[0] * J3p[0] * iE3;
+      B.Hpp[1] += J3p[0] * J3p[1] * iE3;
+      B.Hpp[2] += J3p[1] * J3p[1] * iE3;
+      B.Hpp[3] += J3p[0] * J3p[2] * iE3;
+      B.Hpp[4] += J3p[1] * J3p[2] * iE3;
+      B.Hpp[5] += J3p[2] * J3p[2] * iE3;
+      if (!ls) {  // multiplier-weighted constraint Hessians
+        const int r1 = 2 * (D.KV * p + k);
+        const double y1 = s1 * yd[r1], y3 = scI[r1 + 1] * yd[r1 + 1];
+        y1sum += y1;
+        for (int j = 0; j < NZ; ++j) {
+          B.B[j][0] += y3 * G.A0[j];
+          B.B[j][1] += y3 * G.A1[j];
+          B.B[j][2] += y3 * (G.A0[j] * dv[0] + G.A1[j] * dv[1]);
+        }
+        B.Hpp[5] -= y3 * (G.w0 * rv[0] + G.w1 * rv[1]);
+      }
+    }
+    if (!ls)
+      for (int r = 0; r < NZ; ++r)
+        for (int q = 0; q <= r; ++q) B.K[B.pk(r, q)] += y1sum * 2.0 * (G.A0[r] * G.A0[q] + G.A1[r] * G.A1[q]);
+    for (int j = 0; j < NZ; ++j) {
+      double dg;
+      if (j >= G.em || ls) {
+        dg = 1.0;  // padding / least-squares identity
+      } else {
+        const int vi = G.la0 + j;
+        dg = zL[vi] / (x[vi] - xL[vi]) + zU[vi] / (xU[vi] - x[vi]) + dw;
+      }
+      B.K[B.pk(j, j)] += dg;
+    }
+  }
+
+  __attribute__((noinline)) HTP_HD void local_pivoted_pt(int p, bool ls, double dw, double dc, double* V, int nrhs,
+                                                         int* inertia) const {
+    PtGeom G;
+    pt_geom(A(L.x), p, G);
+    PtBlock<EM_> B;
+    build_local_pt(B, G, p, ls, dw, dc);
+    int ip[EM_];
+    bk_factor_packed(B.K, ip, EM_, inertia[0], inertia[1]);
+    for (int k = 0; k < nrhs; ++k) bk_solve_packed(B.K, ip, EM_, V + k * EM_);
+  }
+
+  HTP_HD HTP_FI void local_factor_sweep_pt(bool ls, double dw, double dc, int& neg, int& zero) {
+    gd* PS = A(L.pairS);
+    const gd* x = A(L.x);
+    constexpr int NZ = EM_;
+    for (int p = c.lane; p < D.P; p += c.width) {
+      PtGeom G;
+      pt_geom(x, p, G);
+      PtBlock<EM_> B;
+      build_local_pt(B, G, p, ls, dw, dc);
+      B.factor();
+      double Vp[3 * NZ];
+      int bneg = B.neg, bzero = B.zero;
+      if (B.piv) {
+        for (int col = 0; col < 3; ++col)
+          for (int r = 0; r < NZ; ++r) Vp[col * NZ + r] = B.B[r][col];
+        int pn[2];
+        local_pivoted_pt(p, ls, dw, dc, Vp, 3, pn);
+        bneg = pn[0];
+        bzero = pn[1];
+      }
+      neg += bneg;
+      zero |= bzero;
+      double S[6] = {0, 0, 0, 0, 0, 0};
+      for (int col = 0; col < 3; ++col) {
+        double v[NZ];
+        for (int r = 0; r < NZ; ++r) v[r] = B.piv ? Vp[col * NZ + r] : B.B[r][col];
+        if (!B.piv) B.solve(v);
+        for (int row = 0; row <= col; ++row) {
+          double acc = 0.0;
+          for (int r = 0; r < NZ; ++r) acc += B.B[r][row] * v[r];
+          const int idx = (col == 0) ? 0 : (col == 1 ? (row == 0 ? 1 : 2) : (row == 0 ? 3 : (row == 1 ? 4 : 5)));
+          S[idx] = acc;
+        }
+      }
+      for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
+    }
+  }
+
+  // z-part rhs of block p: bx + sum_rows J_z q_r (q_r = (bd + bs/Ds)/E); J3p q3 summed into pp
+  HTP_HD HTP_FI void pt_rhs(const PtGeom& G, int p, bool ls, double dw, double dc, const gd* bx, const gd* bs,
+                            const gd* bd, double* v, double* pp) const {
+    for (int j = 0; j < EM_; ++j) v[j] = (j < G.em) ? bx[G.la0 + j] : 0.0;
+    pp[0] = pp[1] = pp[2] = 0.0;
+    double Aw2[EM_];
+    for (int j = 0; j < EM_; ++j) Aw2[j] = 2.0 * (G.A0[j] * G.w0 + G.A1[j] * G.w1);
+    for (int k = 0; k < D.KV; ++k) {
+      double Ds1, E1, Ds3, E3, s1, J3z[EM_], J3p[3], dv[2], rv[2];
+      pt_row_e(p, k, ls, dw, dc, Ds1, E1, Ds3, E3);
+      pt_row_jac(G, p, k, s1, J3z, J3p, dv, rv);
+      const int r1 = 2 * (D.KV * p + k), r3 = r1 + 1;
+      const double q1 = (bd[r1] + bs[r1] / Ds1) / E1;
+      const double q3 = (bd[r3] + bs[r3] / Ds3) / E3;
+      for (int j = 0; j < EM_; ++j) v[j] += s1 * Aw2[j] * q1 + J3z[j] * q3;
+      for (int col = 0; col < 3; ++col) pp[col] += J3p[col] * q3;
+    }
+  }
+
+  HTP_HD HTP_FI void local_rhs_sweep_pt(bool ls, double dw, double dc, const gd* bx, const gd* bs, const gd* bd) {
+    gd* PR = A(L.pairR);
+    const gd* x = A(L.x);
+    constexpr int NZ = EM_;
+    for (int p = c.lane; p < D.P; p += c.width) {
+      PtGeom G;
+      pt_geom(x, p, G);
+      PtBlock<EM_> B;
+      build_local_pt(B, G, p, ls, dw, dc);
+      B.factor();
+      double v[NZ], pp[3];
+      pt_rhs(G, p, ls, dw, dc, bx, bs, bd, v, pp);
+      if (B.piv) {
+        int pn[2];
+        local_pivoted_pt(p, ls, dw, dc, v, 1, pn);
+      } else {
+        B.solve(v);
+      }
+      for (int col = 0; col < 3; ++col) {
+        double acc = 0.0;
+        for (int r = 0; r < NZ; ++r) acc += B.B[r][col] * v[r];
+        PR[3 * p + col] = -acc + pp[col];
+      }
+    }
+  }
+
+  HTP_HD HTP_FI void local_back_sweep_pt(bool ls, double dw, double dc, const gd* bx, const gd* bs, const gd* bd,
+                                         gd* ox, gd* os, gd* od) {
+    const gd* x = A(L.x);
+    constexpr int NZ = EM_;
+    for (int p = c.lane; p < D.P; p += c.width) {
+      PtGeom G;
+      pt_geom(x, p, G);
+      PtBlock<EM_> B;
+      build_local_pt(B, G, p, ls, dw, dc);
+      B.factor();
+      double v[NZ], pp[3];
+      pt_rhs(G, p, ls, dw, dc, bx, bs, bd, v, pp);
+      const double dp[3] = {ox[NS * G.i], ox[NS * G.i + 1], ox[NS * G.i + 3]};
+      for (int r = 0; r < NZ; ++r) v[r] -= B.B[r][0] * dp[0] + B.B[r][1] * dp[1] + B.B[r][2] * dp[2];
+      if (B.piv) {
+        int pn[2];
+        local_pivoted_pt(p, ls, dw, dc, v, 1, pn);
+      } else {
+        B.solve(v);
+      }
+      for (int j = 0; j < EM_; ++j)
+        if (j < G.em) ox[G.la0 + j] = v[j];
+      double Aw2[EM_];
+      for (int j = 0; j < EM_; ++j) Aw2[j] = 2.0 * (G.A0[j] * G.w0 + G.A1[j] * G.w1);
+      for (int k = 0; k < D.KV; ++k) {
+        double Ds1, E1, Ds3, E3, s1, J3z[EM_], J3p[3], dv[2], rv[2];
+        pt_row_e(p, k, ls, dw, dc, Ds1, E1, Ds3, E3);
+        pt_row_jac(G, p, k, s1, J3z, J3p, dv, rv);
+        const int r1 = 2 * (D.KV * p + k), r3 = r1 + 1;
+        double j1 = 0.0, j3 = J3p[0] * dp[0] + J3p[1] * dp[1] + J3p[2] * dp[2];
+        for (int j = 0; j < EM_; ++j) {
+          j1 += s1 * Aw2[j] * v[j];
+          j3 += J3z[j] * v[j];
+        }
+        const double y1 = (j1 - bd[r1] - bs[r1] / Ds1) / E1;
+        const double y3 = (j3 - bd[r3] - bs[r3] / Ds3) / E3;
+        od[r1] = y1;
+        od[r3] = y3;
+        os[r1] = (bs[r1] + y1) / Ds1;
+        os[r3] = (bs[r3] + y3) / Ds3;
+      }
+    }
+  }
+
+  // terminal block of the point formulation (stage-chain block N): rows
+  // X_{N-1} - end = 0 (optimizer_points.py:273-278), coupled to x_{N-1}
+  HTP_HD HTP_FI void assemble_term_pt(double dc) {
+    const int N = D.N, nb = D.nb;
+    const gd* scE = A(L.scE);
+    gd* K = A(L.Kst) + (int64_t)N * nb * nb;
+    gd* O = A(L.Off) + (int64_t)N * nb * nb;
+    for (int q = c.lane; q < nb * nb; q += c.width) {
+      const int r = q / nb, cc = q % nb;
+      K[q] = (r == cc) ? (r < NS ? -dc : 1.0) : 0.0;
+      O[q] = (r < NS && cc == NS + r) ? scE[D.eTerm + r] : 0.0;
     }
   }
 
@@ -989,7 +1443,20 @@ struct ObcaSolver {
       add(NS + a, NS + a, dg);
     }
     for (int a = nv; a < D.nw; ++a) add(NS + a, NS + a, 1.0);  // padding (last stage)
+    if (PT && !ls && i < N - 1) {  // optimizer_points.py objective: 20 (v dT)^2, (u_{i+1} - u_i)^2
+      const int U0 = NS + 5, V0 = NS + 2;
+      add(V0, V0, sf * 40.0 * dT * dT);
+      if (i < N - 2) {
+        add(U0, U0, sf * 2.0);
+        add(U0 + 1, U0 + 1, sf * 2.0);
+      }
+      if (i >= 1) {
+        add(U0, U0, sf * 2.0);
+        add(U0 + 1, U0 + 1, sf * 2.0);
+      }
+    }
     if (!ls && i < N - 1) {
+      if constexpr (!PT) {
       const double tau = tauv(x, i), h = dT * tau;
       const double Qs00 = 2 * par(P_Q00), Qs01 = par(P_Q01) + par(P_Q10), Qs11 = 2 * par(P_Q11);
       const double Rs00 = 2 * par(P_R00), Rs01 = par(P_R01) + par(P_R10), Rs11 = 2 * par(P_R11);
@@ -1024,6 +1491,7 @@ struct ObcaSolver {
         add(U0 + 1, U0, sf * Rs01 * ih2);
         add(U0 + 1, U0 + 1, sf * Rs11 * ih2);
       }
+      }
       // dynamics Hessian of interval i:  sum_k (-yhat_k) d2F_k
       double w[8], H[36], yy[5];
       stage_w(x, i, w);
@@ -1035,9 +1503,9 @@ struct ObcaSolver {
       // last stage has no u; nothing else
     }
     // local-block Schur complements on (x, y, theta)
-    const int MK = D.M * D.K;
+    const int MK = blocks_per_stage();
     for (int q = 0; q < MK; ++q) {
-      const gd* S = PS + 6 * (i * MK + q);
+      const gd* S = PS + 6 * blk(i, q);
       add(NS + 0, NS + 0, S[0]);
       add(NS + 1, NS + 0, S[1]);
       add(NS + 1, NS + 1, S[2]);
@@ -1046,7 +1514,7 @@ struct ObcaSolver {
       add(NS + 3, NS + 3, S[5]);
     }
     // terminal slack block (i == N-1): Hs = 10000 sf + dw
-    if (i == N - 1) {
+    if (!PT && i == N - 1) {
       const double Hs = ls ? 1.0 : 10000.0 * sf + dw;
       for (int k = 0; k < NS; ++k) {
         const double st = scE[D.eTerm + k];
@@ -1065,7 +1533,12 @@ struct ObcaSolver {
         const double s_ = scE[D.eDyn + NS * i + k];
         for (int j = 0; j < D.nw; ++j) O[k * nb + NS + j] = -s_ * J[k * D.nw + j];
       }
-      if (!ls && i < N - 2) {
+      if (PT && !ls && i < N - 2) {
+        const int U0 = NS + 5;
+        O[U0 * nb + U0] = -sf * 2.0;
+        O[(U0 + 1) * nb + U0 + 1] = -sf * 2.0;
+      }
+      if (!PT && !ls && i < N - 2) {
         const double tau = tauv(x, i), h = dT * tau, ih2 = 1.0 / (h * h);
         const double Rs00 = 2 * par(P_R00), Rs01 = par(P_R01) + par(P_R10), Rs11 = 2 * par(P_R11);
         const int U0 = NS + 5, T0 = NS + 7;
@@ -1643,17 +2116,19 @@ struct ObcaSolver {
     // Bunch-Kaufman path below.
     // (A zero local pivot only needs reporting: IPOPT's reaction -- dc, then
     // dw -- does not depend on the stage system.)
-    if (zero > 0 || neg != 2 * D.P) {
+    if (zero > 0 || neg != (PT ? 0 : 2 * D.P)) {
       use_ric = false;
       neg_out = -1;
       zero_out = zero;
       return;
     }
     for (int i = c.lane; i < N; i += c.width) assemble_stage(i, ls, dw, dc);
+    if constexpr (PT) assemble_term_pt(dc);
     c.sync();
     long long t2 = c.clock();
     cyc[1] += t2 - t1;
-    if (dc == 0.0) {
+    // (the point formulation's hard terminal rows have no Riccati form: block LDL^T)
+    if (!PT && dc == 0.0) {
       const int bad = riccati_factor();
       use_ric = true;
       cyc[2] += c.clock() - t2;
@@ -1672,7 +2147,7 @@ struct ObcaSolver {
     li* ipc = c.ildsp;
     int sneg = 0, szero = 0;
     const int nb2 = nb * nb;
-    for (int i = 0; i < N; ++i) {
+    for (int i = 0; i < D.nblk; ++i) {
       const gd* K = A(L.Kst) + (int64_t)i * nb2;
       for (int e = c.lane; e < nb2; e += c.width) Acur[e] = K[e];
       if (i > 0) {
@@ -1709,7 +2184,7 @@ struct ObcaSolver {
 #ifdef HTP_HOST_DEBUG
     printf("[dbg]   pairs neg=%d (exp %d) zero=%d stages neg=%d (exp %d) zero=%d\n", neg, 2 * D.P, zero, sneg, NS * N, szero);
 #endif
-    neg_out = neg + sneg + NS + D.md;
+    neg_out = neg + sneg + (PT ? 0 : NS) + D.md;
     zero_out = zero + szero;
   }
 
@@ -1723,7 +2198,7 @@ struct ObcaSolver {
     const gd* PR = A(L.pairR);
     const gd* scE = A(L.scE);
     gd* V = A(L.V);
-    const int MK = D.M * D.K;
+    const int MK = blocks_per_stage();
     const double Hs = ls ? 1.0 : 10000.0 * sf + dw;
     for (int i = c.lane; i < N; i += c.width) {
       gd* r = V + (int64_t)i * nb;
@@ -1736,26 +2211,29 @@ struct ObcaSolver {
         if (D.topt) r[NS + 7] = bx[D.oTAU + i];
       } else {
         for (int a = NS; a < D.nw; ++a) r[NS + a] = 0.0;
-        for (int k = 0; k < NS; ++k) {
-          const double st = scE[D.eTerm + k];
-          const double Et = dc + st * st / Hs;
-          r[NS + k] -= st / Et * (st * bx[D.oS + k] / Hs - bc[D.eTerm + k]);
-        }
+        if constexpr (!PT)
+          for (int k = 0; k < NS; ++k) {
+            const double st = scE[D.eTerm + k];
+            const double Et = dc + st * st / Hs;
+            r[NS + k] -= st / Et * (st * bx[D.oS + k] / Hs - bc[D.eTerm + k]);
+          }
       }
       for (int q = 0; q < MK; ++q) {
-        const int p = i * MK + q;
+        const int p = blk(i, q);
         r[NS + 0] += PR[3 * p];
         r[NS + 1] += PR[3 * p + 1];
         r[NS + 3] += PR[3 * p + 2];
       }
     }
+    if constexpr (PT)
+      for (int e = c.lane; e < nb; e += c.width) V[(int64_t)N * nb + e] = (e < NS) ? bc[D.eTerm + e] : 0.0;
     c.sync();
     gd* X = A(L.X);
     if (use_ric) {
       riccati_solve(V, X);
     } else {
     // forward: V_i -= LD_i V_{i-1}
-    for (int i = 1; i < N; ++i) {
+    for (int i = 1; i < D.nblk; ++i) {
       const gd* LD = A(L.LD) + (int64_t)i * nb * nb;
       gd* vi = V + (int64_t)i * nb;
       const gd* vp = V + (int64_t)(i - 1) * nb;
@@ -1768,12 +2246,12 @@ struct ObcaSolver {
     }
     // backward: X_i = Dinv_i (V_i - Off_{i+1}' X_{i+1})
     ld* tv = c.lds + 3 * NBMAX * NBMAX;
-    for (int i = N - 1; i >= 0; --i) {
+    for (int i = D.nblk - 1; i >= 0; --i) {
       gd* xi = X + (int64_t)i * nb;
       const gd* vi = V + (int64_t)i * nb;
       for (int r = c.lane; r < nb; r += c.width) {
         double acc = vi[r];
-        if (i < N - 1) {
+        if (i < D.nblk - 1) {
           const gd* O = A(L.Off) + (int64_t)(i + 1) * nb * nb;
           const gd* xn = X + (int64_t)(i + 1) * nb;
           for (int t = 0; t < nb; ++t) acc -= O[t * nb + r] * xn[t];
@@ -1800,6 +2278,8 @@ struct ObcaSolver {
         ox[D.oU + NC * i] = xi[NS + 5];
         ox[D.oU + NC * i + 1] = xi[NS + 6];
         if (D.topt) ox[D.oTAU + i] = xi[NS + 7];
+      } else if constexpr (PT) {
+        for (int k = 0; k < NS; ++k) oc[D.eTerm + k] = X[(int64_t)N * nb + k];
       } else {
         for (int k = 0; k < NS; ++k) {
           const double st = scE[D.eTerm + k];
@@ -1905,6 +2385,7 @@ struct ObcaSolver {
     for (int r = c.lane; r < D.md; r += c.width) {
       const double g = dd[r] / scI[r];
       if ((r & 1) == 0) v = dmax(v, dmax(0.0 - g, g - 1.0));
+      else if (PT) v = dmax(v, dmax(dmn - g, g - 100000.0));
       else v = dmax(v, dmn - g);
     }
     return c.maxv(v);
@@ -2402,6 +2883,7 @@ struct ObcaSolver {
         if ((q - D.oU) % 2 == 0) { lo = -amax; hi = amax; } else { lo = -wmax; hi = wmax; }
       } else if (q < D.oTAU) {
         lo = 0.0;
+        if (PT) hi = 100000.0;
       } else if (q < D.oS) {
         lo = 0.05 / par(P_DT); hi = 1.0;
       }

@@ -68,3 +68,20 @@ def polygon_exterior_vertices(poly):
     if a.shape[0] > 1 and np.all(a[0] == a[-1]):
         a = a[:-1]
     return a
+
+
+def convex_hull_ring(points):
+    """Vertices of conv(points) as shapely's `MultiPoint(points).convex_hull.exterior.coords[:-1]`
+    (GEOS ConvexHull: Graham scan from the lowest point -- minimum y, then minimum x -- clockwise,
+    collinear points dropped).  Used by optimizer_points.get_vehicle_vertices (:35-50)."""
+    H = _hull(points)                 # counter-clockwise, collinear points removed
+    start = min(range(len(H)), key=lambda k: (H[k][1], H[k][0]))
+    ccw = np.roll(H, -start, axis=0)
+    return np.vstack([ccw[:1], ccw[:0:-1]])  # same start, clockwise
+
+
+def vehicle_hull_vertices(polys):
+    """get_vehicle_vertices(car, convex_hull=True) (optimizer_points.py:35-50): the rear-axle
+    origin plus every body / implement polygon vertex, convex hull."""
+    pts = [np.zeros((1, 2))] + [polygon_exterior_vertices(p) for p in polys]
+    return convex_hull_ring(np.vstack(pts))

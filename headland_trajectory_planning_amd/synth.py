@@ -244,6 +244,32 @@ def make_instance(pid, N=80, M=6, implement="none", key=20251015, **over):
     return inst
 
 
+def make_points_instance(pid, N=80, M=6, implement="none", key=20251015, **over):
+    """The same synthetic headland turn in the point formulation (oracle/nlp_points.py instance
+    format, R/obca_py/optimizer_points.py): obstacle halfspaces, vehicle hull vertices
+    (get_vehicle_vertices :35-50), the reference's default x/y bounds (initialize_manual :52-62)."""
+    base = make_instance(pid, N=N, M=M, implement=implement, key=key)
+    veh = VEHICLE
+    # hard start/end constraints (no terminal slack): give the turn time enough to be feasible
+    # (cruise <= 0.5 m/s, MAX_VELOCITY 1, MAX_ACCEL 1, MAX_STEER_RATE 0.7)
+    ds = base["meta"]["length"] / (N - 1)
+    dT = float(over.get("dT", max(base["dT"], ds / 0.5)))
+    traj = base["init_traj"].copy()
+    traj[1:-1, 2] = ds / dT
+    polys = [geometry.body_rectangle(veh["axle_to_front"], veh["axle_to_back"], veh["width"])]
+    if IMPLEMENTS[implement] is not None:
+        polys.append(geometry.implement_rectangle(IMPLEMENTS[implement]))
+    inst = dict(
+        init_traj=traj, obs_A=base["obs_A"], obs_b=base["obs_b"], obstacles=base["obstacles"],
+        vertices=geometry.vehicle_hull_vertices(polys), dT=dT, wheelbase=veh["wheelbase"],
+        max_steer=veh["max_steer"], max_velocity=1.0, max_accel=1.0, max_steer_rate=0.7, min_dist=0.1,
+        x_bound=[-9999999.0, 9999999.0], y_bound=[-9999999.0, 9999999.0], meta=base["meta"],
+    )
+    for kk, vv in over.items():
+        inst[kk] = vv
+    return inst
+
+
 CONFIGS = {
     # name: (batch, N, M, implement)  -- BASELINE.json configs[0..4]
     "A": (1, 40, 2, "none"),

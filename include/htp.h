@@ -95,6 +95,34 @@ double htp_last_kernel_ms(htp_ctx* ctx);
 int htp_last_cycles(htp_ctx* ctx, int64_t* out, int32_t batch);
 
 /* ---------------------------------------------------------------------------
+ * Point formulation (R/obca_py/optimizer_points.py OBCAOptimizer: initialize_manual
+ * :52-108, generate_object :193-227, generate_variable :229-255, generate_constrain
+ * :257-327, solve :157-191): lambda-only duals, one distance row per vehicle hull
+ * vertex, hard start/end states, objective sum du^2 + 20 (v dT)^2.  Same solver,
+ * batched; x in optimizer_points.py's variable order (X, U, LAMBDA obstacle-major).
+ * Parameters: HTP_P_DT, _WHEELBASE, _MAXSTEER, _MAXV (MAX_VELOCITY), _MAXACC,
+ * _MAXSR (MAX_STEER_RATE), _DMIN (MIN_DISTANCE_TO_OBS), _XLO.._YHI (min/max x/y);
+ * the Q/R/W slots are ignored (the reference never reads r, q). */
+typedef struct {
+  int32_t batch, N, M, n_vertices;
+  const int32_t* obs_edges;   /* [M] halfspaces of each obstacle = len(obstacle) (<= 8) */
+  const double* traj;         /* [batch][N][5] init_guess_path */
+  const double* obs_A;        /* [batch][sum obs_edges][2] compute_polytope_halfspaces A */
+  const double* obs_b;        /* [batch][sum obs_edges]                                 */
+  const double* vertices;     /* [batch][n_vertices][2] get_vehicle_vertices (:35-50)   */
+  const double* params;       /* [batch][HTP_NPARAM]                                    */
+  const double* init_control; /* nullable [batch][N-1][2]                               */
+} htp_obca_points_batch;
+
+int htp_obca_points_sizes(int32_t N, int32_t M, int32_t n_vertices, const int32_t* obs_edges, int64_t* n_var,
+                          int64_t* n_eq, int64_t* n_ineq, int64_t* ws_doubles);
+/* host buffers in/out (synchronous) */
+int htp_obca_points_solve_batch(htp_ctx* ctx, const htp_obca_points_batch* in, htp_obca_result* out);
+/* device-resident buffers, enqueued on `stream`; timing via htp_last_kernel_ms */
+int htp_obca_points_solve_batch_device(htp_ctx* ctx, const htp_obca_points_batch* in, htp_obca_result* out,
+                                       void* stream);
+
+/* ---------------------------------------------------------------------------
  * Reeds-Shepp: all admissible paths between pose pairs, sampled
  * (R/path_planner/utils/reeds_shepp.py calc_all_paths :39-65, called by
  * hybrid_a_star_search.py:248 and safety_forward_path_plan.py:368).

@@ -39,6 +39,24 @@ def lib():
     return _lib
 
 
+def solve_points(insts, options=None):
+    """Point formulation (optimizer_points.py) through the serial host build."""
+    L = lib()
+    L.htp_hostsim_obca_points_solve.argtypes = [ctypes.POINTER(_native.ObcaPointsBatch),
+                                                ctypes.POINTER(_native.ObcaResult), ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_int]
+    L.htp_hostsim_obca_points_solve.restype = ctypes.c_int
+    pk = _native.PointsPackedBatch(insts)
+    res = _native.HostResults(pk.batch, pk.n_var)
+    opts = options or {}
+    names = (ctypes.c_char_p * max(1, len(opts)))(*[k.encode() for k in opts])
+    vals = (ctypes.c_double * max(1, len(opts)))(*[float(v) for v in opts.values()])
+    b, r = pk.struct(), res.struct()
+    rc = L.htp_hostsim_obca_points_solve(ctypes.byref(b), ctypes.byref(r), names, vals, len(opts))
+    assert rc == 0, rc
+    return res
+
+
 def solve(insts, options=None):
     pk = _native.PackedBatch(insts)
     res = _native.HostResults(pk.batch, pk.n_var)

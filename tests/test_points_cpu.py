@@ -1,0 +1,117 @@
+"""Point formulation (R/obca_py/optimizer_points.py): oracle derivatives, the
+solver core's host build against the oracle IPM, and the drop-in shim surface
+(CPU only; the GPU parity tests are in test_gpu_points.py).
+
+Parity anchor: the reference has no test or fixture for optimizer_points.py
+and CasADi is absent here, so the oracle (oracle/nlp_points.py + the IPOPT
+restatement oracle/ipm.py) is "parity unpinned" against CasADi; its
+derivatives are pinned by finite differences below."""
+import numpy as np
+import pytest
+
+import _hostsim as H
+from headland_trajectory_planning_amd import geometry, synth
+from headland_trajectory_planning_amd.obca_py.car_model_obca import CarModel
+from headland_trajectory_planning_amd.obca_py.optimizer_points import OBCAOptimizer
+from oracle.ipm import IpoptRestatement
+from oracle.nlp_points import PointNLP
+
+
+def _fd(fun, x, e=1e-6):
+    cols = []
+    for k in range(x.size):
+        d = np.zeros_like(x)
+        d[k] = e
+        cols.append((fun(x + d) - fun(x - d)) / (2 * e))
+    return np.array(cols).T
+
+
+def test_oracle_derivatives_match_finite_differences():
+    nlp = PointNLP(synth.make_points_instance(3, N=6, M=2, implement="mower"))
+    rng = np.random.default_rng(0)
+    x = nlp.x0 + 0.05 * rng.standard_normal(nlp.n)
+    assert np.max(np.abs(nlp.grad_f(x) - _fd(lambda z: np.array([nlp.f(z)]), x)[0])) < 1e-6
+    assert np.max(np.abs(nlp.jac(x).toarray() - _fd(nlp.cons, x))) < 1e-6
+    y = rng.standard_normal(nlp.m)
+    H_ = nlp.hess(x, y, 0.7).toarray()
+    Hf = _fd(lambda z: 0.7 * nlp.grad_f(z) + nlp.jac(z).T @ y, x)
+    assert np.max(np.abs(H_ - Hf)) < 1e-5
+    assert np.max(np.abs(H_ - H_.T)) < 1e-12
+
+
+def test_oracle_layout_follows_reference():
+    inst = synth.make_points_instance(0, N=8, M=3)
+    nlp = PointNLP(inst)
+    KV = inst["vertices"].shape[0]
+    assert nlp.n == 5 * 8 + 2 * 7 + 8 * 12
+    assert nlp.counts() == {"n_var": nlp.n, "n_eq": 5 * 9, "n_ineq": 2 * KV * 8 * 3}
+    # LAMBDA obstacle-major: block (j, i) starts at N * sum_{j'<j} n_j' + i * n_j (:294-296)
+    assert [b[2] - nlp.oLAM for b in nlp.blocks[:3]] == [0, 4, 8]
+    assert nlp.blocks[8][2] - nlp.oLAM == 8 * 4
+    assert np.all(nlp.x0[nlp.oLAM:] == 0.1)
+    assert np.all(nlp.x_U[nlp.oLAM:] == 100000.0)
+
+
+CASES = [("pid0", dict(pid=0, N=12, M=2)), ("pid1", dict(pid=1, N=12, M=2)),
+         ("mower", dict(pid=5, N=10, M=2, implement="mower"))]
+
+
+@pytest.mark.parametrize("name,kw", CASES, ids=[c[0] for c in CASES])
+def test_host_core_matches_oracle(name, kw):
+    kw = dict(kw)
+    inst = synth.make_points_instance(kw.pop("pid"), **kw)
+    ref = IpoptRestatement(PointNLP(inst)).solve()
+    h = H.solve_points([inst])
+    assert ref["status_str"] == "Solve_Succeeded"
+    assert h.status[0] == 0 and h.iterations[0] == ref["iters"]
+    assert np.max(np.abs(h.x[0] - ref["x"])) < 1e-8
+    assert abs(h.objective[0] - ref["f"]) <= 1e-9 * abs(ref["f"])
+
+
+def test_host_core_matches_oracle_mixed_edges_and_init_control():
+    inst = synth.make_points_instance(6, N=10, M=3)
+    A, b = geometry.polytope_halfspaces(np.array([[60.0, 60.0], [62.0, 60.0], [61.0, 62.0]]))
+    inst["obs_A"][2], inst["obs_b"][2] = A, b
+    inst["init_control"] = 0.05 * np.random.default_rng(1).standard_normal((9, 2))
+    ref = IpoptRestatement(PointNLP(inst)).solve()
+    h = H.solve_points([inst])
+    assert h.status[0] == 0 and h.iterations[0] == ref["iters"]
+    assert np.max(np.abs(h.x[0] - ref["x"])) < 1e-7
+
+
+def test_hull_vertices_follow_geos_order():
+    # shapely: MultiPoint([(0,0),(1,0),(1,1),(0,1)]).convex_hull -> ((0 0, 0 1, 1 1, 1 0, 0 0))
+    assert np.array_equal(geometry.convex_hull_ring(np.array([[0, 0], [1, 0], [1, 1], [0, 1.0]])),
+                          [[0, 0], [0, 1], [1, 1], [1, 0]])
+    car = CarModel(max_steer=0.55, axle_to_back=0.55, width=1.48, aux_poly_features=[synth.MOWER], with_aux=True)
+    V = geometry.vehicle_hull_vertices([car.car_poly] + car.aux_polys)
+    assert V[0][1] == np.min(V[:, 1])
+    e1, e2 = np.roll(V, -1, 0) - V, np.roll(V, -2, 0) - np.roll(V, -1, 0)
+    cross = e1[:, 0] * e2[:, 1] - e1[:, 1] * e2[:, 0]
+    assert np.all(cross < 0)  # clockwise, strictly convex
+
+
+def test_shim_surface_matches_reference(capsys):
+    inst = synth.make_points_instance(2, N=10, M=2)
+    car = CarModel(max_steer=0.55, axle_to_back=0.55, width=1.48)
+    opt = OBCAOptimizer(car, dT=inst["dT"])
+    obs = [np.asarray(o) for o in inst["obstacles"]]
+    opt.initialize_manual(inst["init_traj"], obs)
+    out = capsys.readouterr().out
+    assert "number of constraints for obstacle free:  40 number of variables:  95" in out
+    assert opt.build_model()
+    opt.generate_object(np.eye(2), np.eye(5))
+    opt.generate_variable()
+    opt.generate_constrain()
+    mine = opt.instance()
+    nlp = PointNLP(mine)
+    assert len(opt.lbx) == len(opt.ubx) == nlp.n
+    assert np.allclose(opt.lbx, nlp.x_L) and np.allclose(opt.ubx, nlp.x_U)
+    assert np.allclose(opt.lbg, nlp.g_L) and np.allclose(opt.ubg, nlp.g_U)
+    assert np.allclose(opt.x0, nlp.x0)
+    closed = [np.vstack([o, o[:1]]) for o in obs]
+    opt2 = OBCAOptimizer(car, dT=inst["dT"])
+    opt2.initialize_manual(inst["init_traj"], closed)
+    opt2.build_model()
+    with pytest.raises(ValueError):
+        opt2.generate_constrain()
