@@ -1,0 +1,80 @@
+"""Point-formulation OBCA throughput (R/obca_py/optimizer_points.py):
+B seeded headland turns of the config-B shape (N=80, 6 quad obstacles, body hull)
+solved in one launch, inputs resident in HBM, kernel time from hipEvents
+(htp_last_kernel_ms).  CPU baseline: the oracle (numpy IPOPT restatement over a
+dense KKT, 1 core) on a bounded sample at N=20 (the dense oracle is too slow at
+N=80), reported as such.  Prints one JSON line."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--N", type=int, default=80)
+    ap.add_argument("--M", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=2)
+    args = ap.parse_args()
+    import torch
+
+    from headland_trajectory_planning_amd import _native, synth
+    dev = torch.device("cuda", 0)
+    t0 = time.time()
+    uniq = [synth.make_points_instance(pid, N=args.N, M=args.M) for pid in range(min(args.batch, 512))]
+    insts = [uniq[i % len(uniq)] for i in range(args.batch)]
+    pk = _native.PointsPackedBatch(insts)
+    gen_s = time.time() - t0
+    B = pk.batch
+    names = ("traj", "obs_A", "obs_b", "vertices", "params")
+    dv = {n: torch.from_numpy(np.ascontiguousarray(getattr(pk, n))).to(dev) for n in names}
+    out = {"x": torch.empty((B, pk.n_var), dtype=torch.float64, device=dev),
+           "objective": torch.empty(B, dtype=torch.float64, device=dev),
+           "status": torch.empty(B, dtype=torch.int32, device=dev),
+           "iterations": torch.empty(B, dtype=torch.int32, device=dev),
+           "n_factor": torch.empty(B, dtype=torch.int32, device=dev),
+           "nlp_error": torch.empty(B, dtype=torch.float64, device=dev)}
+    ctx = _native.Context(0)
+    b = pk.struct({k: v.data_ptr() for k, v in dv.items()})
+    r = _native.ObcaResult(*[out[k].data_ptr() for k in ("x", "objective", "status", "iterations", "n_factor",
+                                                          "nlp_error")])
+    stream = torch.cuda.current_stream().cuda_stream
+    ms = []
+    for it in range(args.steps + 1):
+        assert ctx.lib.htp_obca_points_solve_batch_device(ctx.ctx, ctypes.byref(b), ctypes.byref(r), stream) == 0
+        torch.cuda.synchronize()
+        if it:
+            ms.append(ctx.last_kernel_ms())
+        print(f"[bench_points] step {it} {ctx.last_kernel_ms():.1f} ms", file=sys.stderr, flush=True)
+    kms = float(np.mean(ms))
+    st = out["status"].cpu().numpy()
+    iters = out["iterations"].cpu().numpy()
+    from oracle.ipm import IpoptRestatement
+    from oracle.nlp_points import PointNLP
+    t = time.perf_counter()
+    cit = 0
+    for pid in range(args.cpu_sample):
+        res = IpoptRestatement(PointNLP(synth.make_points_instance(pid, N=20, M=args.M))).solve()
+        cit += res["iters"]
+    cpu_s = time.perf_counter() - t
+    print(json.dumps({"metric": "point-formulation OBCA solves/s", "value": B / (kms / 1e3), "unit": "solves/s",
+                      "batch": B, "N": args.N, "M": args.M, "n_vertices": pk.n_vertices, "kernel_ms": kms,
+                      "success_rate": float(np.mean(np.isin(st, (0, 1)))), "mean_iters": float(iters.mean()),
+                      "status_counts": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
+                      "gen_s": gen_s,
+                      "cpu_baseline": {"value": args.cpu_sample / cpu_s, "unit": "solves/s", "cores": 1, "kind": "port",
+                                       "sample": f"{args.cpu_sample} problems at N=20 (dense oracle), {cit} iterations "
+                                                 f"in {cpu_s:.1f} s"}}))
+
+
+if __name__ == "__main__":
+    main()
