@@ -84,7 +84,8 @@ EXPORTS = ["htp_obca_sizes", "htp_create", "htp_destroy", "htp_last_error", "htp
            "htp_rs_all_paths_batch", "htp_rs_all_paths_batch_device", "htp_rs_last_ms",
            "htp_hastar_search_batch", "htp_hastar_search_batch_device", "htp_hastar_last_ms",
            "htp_ypark_search_batch", "htp_ypark_search_batch_device", "htp_ypark_last_ms",
-           "htp_obca_points_sizes", "htp_obca_points_solve_batch", "htp_obca_points_solve_batch_device"]
+           "htp_obca_points_sizes", "htp_obca_points_solve_batch", "htp_obca_points_solve_batch_device",
+           "htp_init_ref_path_batch", "htp_init_ref_path_batch_device", "htp_init_ref_path_last_ms"]
 
 
 def _declare(lib):
@@ -103,6 +104,13 @@ def _declare(lib):
     lib.htp_obca_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ObcaBatch),
                                                 ctypes.POINTER(ObcaResult), ctypes.c_void_p]
     lib.htp_obca_solve_batch_device.restype = ctypes.c_int
+    lib.htp_init_ref_path_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(RpBatch), ctypes.POINTER(RpResult)]
+    lib.htp_init_ref_path_batch.restype = ctypes.c_int
+    lib.htp_init_ref_path_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(RpBatch), ctypes.POINTER(RpResult),
+                                                   ctypes.c_void_p]
+    lib.htp_init_ref_path_batch_device.restype = ctypes.c_int
+    lib.htp_init_ref_path_last_ms.argtypes = [ctypes.c_void_p]
+    lib.htp_init_ref_path_last_ms.restype = ctypes.c_double
     lib.htp_obca_points_sizes.argtypes = [ctypes.c_int32] * 3 + [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int64)] * 4
     lib.htp_obca_points_sizes.restype = ctypes.c_int
     lib.htp_obca_points_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ObcaPointsBatch),
@@ -311,6 +319,64 @@ class PointsPackedBatch:
         for name in ("traj", "obs_A", "obs_b", "vertices", "params", "init_control"):
             setattr(b, name, src[name] if name in src else ptr(getattr(self, name)))
         return b
+
+
+class RpBatch(ctypes.Structure):  # htp_refpath_batch
+    _fields_ = [("batch", ctypes.c_int32), ("cap_points", ctypes.c_int32), ("cap_rows", ctypes.c_int32),
+                ("path_off", ctypes.c_void_p), ("xs", ctypes.c_void_p), ("ys", ctypes.c_void_p),
+                ("dirs", ctypes.c_void_p), ("params", ctypes.c_void_p)]
+
+
+class RpResult(ctypes.Structure):  # htp_refpath_result
+    _fields_ = [("status", ctypes.c_void_p), ("n_rows", ctypes.c_void_p), ("traj", ctypes.c_void_p)]
+
+
+RP_STATUS = {0: "ok", 1: "overflow", 2: "bad_segment", 3: "bad_input"}
+
+
+class RefPathPacked:
+    """CSR batch of warm-start paths for get_init_ref_path (R/obca_py/util.py:62-113).
+    paths: list of (xs, ys, dirs) (yaw / curvature columns are not read by the reference);
+    params: per path (WHEEL_BASE, desired_v, ds)."""
+
+    def __init__(self, paths, params, cap_rows=None):
+        self.batch = len(paths)
+        lens = [len(p[0]) for p in paths]
+        self.path_off = np.zeros(self.batch + 1, dtype=np.int32)
+        self.path_off[1:] = np.cumsum(lens)
+        cat = lambda k: np.ascontiguousarray(np.concatenate([np.asarray(p[k], dtype=np.float64) for p in paths])
+                                             if paths else np.zeros(1))
+        self.xs, self.ys, self.dirs = cat(0), cat(1), cat(2)
+        self.params = np.ascontiguousarray(np.asarray(params, dtype=np.float64).reshape(self.batch, 3))
+        self.cap_points = max(1, max(lens) if lens else 1)
+        if cap_rows is None:  # arc length <= polyline length: ceil(len/ds) + 1 rows per segment, + 1 per segment
+            cap_rows = 1
+            for p, prm in zip(paths, self.params):
+                L = float(np.sum(np.hypot(np.diff(p[0]), np.diff(p[1]))))
+                nseg = 1 + int(np.count_nonzero(np.diff(np.asarray(p[2])) != 0))
+                cap_rows = max(cap_rows, int(np.ceil(L / prm[2])) + 2 * nseg + 2)
+        self.cap_rows = int(cap_rows)
+
+    def struct(self, ptrs=None):
+        b = RpBatch()
+        b.batch, b.cap_points, b.cap_rows = self.batch, self.cap_points, self.cap_rows
+        src = ptrs or {}
+        for name in ("path_off", "xs", "ys", "dirs", "params"):
+            setattr(b, name, src[name] if name in src else getattr(self, name).ctypes.data)
+        return b
+
+
+class RefPathResults:
+    def __init__(self, packed):
+        self.status = np.zeros(packed.batch, dtype=np.int32)
+        self.n_rows = np.zeros(packed.batch, dtype=np.int32)
+        self.traj = np.zeros((packed.batch, packed.cap_rows, 5))
+
+    def struct(self):
+        return RpResult(self.status.ctypes.data, self.n_rows.ctypes.data, self.traj.ctypes.data)
+
+    def path(self, b):
+        return self.traj[b, :self.n_rows[b]].copy()
 
 
 class HostResults:
@@ -540,6 +606,17 @@ class Context:
         if rc != 0:
             raise RuntimeError(f"[htp] htp_obca_points_solve_batch failed: {self.error()}")
         return res
+
+    def init_ref_path(self, packed):
+        """Batched get_init_ref_path (host buffers) -> RefPathResults."""
+        res = RefPathResults(packed)
+        b, r = packed.struct(), res.struct()
+        if self.lib.htp_init_ref_path_batch(self.ctx, ctypes.byref(b), ctypes.byref(r)) != 0:
+            raise RuntimeError(f"[htp] htp_init_ref_path_batch failed: {self.error()}")
+        return res
+
+    def init_ref_path_last_ms(self):
+        return self.lib.htp_init_ref_path_last_ms(self.ctx)
 
     def solve_device(self, packed, dev_ptrs, out_ptrs, stream=None):
         b = packed.struct(dev_ptrs)

@@ -31,6 +31,10 @@ struct htp_ctx {
   void* yp_ws = nullptr;
   size_t yp_ws_bytes = 0;
   hipEvent_t yp_ev0 = nullptr, yp_ev1 = nullptr;
+  // warm start -> initial guess batch (htp_refpath.hip)
+  void* rp_ws = nullptr;
+  size_t rp_ws_bytes = 0;
+  hipEvent_t rp_ev0 = nullptr, rp_ev1 = nullptr;
 };
 
 static inline int fail(htp_ctx* c, const std::string& m) {

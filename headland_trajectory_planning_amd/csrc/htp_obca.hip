@@ -121,6 +121,8 @@ htp_ctx* htp_create(int32_t device) {
   (void)hipEventCreate(&c->ha_ev1);
   (void)hipEventCreate(&c->yp_ev0);
   (void)hipEventCreate(&c->yp_ev1);
+  (void)hipEventCreate(&c->rp_ev0);
+  (void)hipEventCreate(&c->rp_ev1);
   return c;
 }
 
@@ -140,6 +142,9 @@ void htp_destroy(htp_ctx* c) {
   if (c->yp_ws) (void)hipFree(c->yp_ws);
   if (c->yp_ev0) (void)hipEventDestroy(c->yp_ev0);
   if (c->yp_ev1) (void)hipEventDestroy(c->yp_ev1);
+  if (c->rp_ws) (void)hipFree(c->rp_ws);
+  if (c->rp_ev0) (void)hipEventDestroy(c->rp_ev0);
+  if (c->rp_ev1) (void)hipEventDestroy(c->rp_ev1);
   delete c;
 }
 

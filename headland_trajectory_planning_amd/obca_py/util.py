@@ -109,3 +109,30 @@ def get_init_ref_path(car, path_xs, path_ys, path_yaws, path_ks, dirs, desired_v
     ref[0, 2] = 0
     ref[-1, 2] = 0
     return ref
+
+
+def get_init_ref_path_batch(car, paths, desired_v=0.5, ds=0.1, device=0):
+    """get_init_ref_path (util.py:62-113) for many warm-start paths in one HIP launch
+    (include/htp.h htp_init_ref_path_batch; one path per wavefront, no CPU fallback).
+    paths: list of (xs, ys, yaws, ks, dirs) as returned by the planners; returns a list of
+    (rows, 5) arrays [x, y, v, theta, steer].  Raises ValueError where scipy's CubicSpline
+    would (a gear segment with fewer than two distinct points)."""
+    from .. import _native
+    from .optimizer import _context
+    packed = _native.RefPathPacked([(p[0], p[1], p[4]) for p in paths],
+                                   [(car.WHEEL_BASE, desired_v, ds)] * len(paths))
+    res = _context(device).init_ref_path(packed)
+    out = []
+    for b in range(len(paths)):
+        st = int(res.status[b])
+        if st == 2:
+            raise ValueError(f"[init_ref_path] path {b}: a gear segment has fewer than two distinct points")
+        if st != 0:
+            raise RuntimeError(f"[init_ref_path] path {b}: {_native.RP_STATUS.get(st, st)}")
+        out.append(res.path(b))
+    return out
+
+
+def get_init_ref_path_gpu(car, path_xs, path_ys, path_yaws, path_ks, dirs, desired_v=0.5, ds=0.1):
+    """Single-path form of get_init_ref_path_batch (same signature as get_init_ref_path)."""
+    return get_init_ref_path_batch(car, [(path_xs, path_ys, path_yaws, path_ks, dirs)], desired_v, ds)[0]

@@ -123,6 +123,32 @@ int htp_obca_points_solve_batch_device(htp_ctx* ctx, const htp_obca_points_batch
                                        void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Warm start -> OBCA initial guess (R/obca_py/util.py get_init_ref_path :62-113
+ * with cubic_spline.calc_spline_course :92-112): split at gear changes,
+ * re-spline every segment over arc length at ds, v = gear * desired_v,
+ * steer = atan(L kappa) (sign-flipped in reverse), headings unwrapped,
+ * v = 0 at both ends.  One path per wavefront.  Only xs, ys and dirs are read
+ * (the reference ignores the yaw and curvature columns). */
+enum { HTP_RP_OK = 0, HTP_RP_OVERFLOW = 1 /* n_rows = rows needed so far */, HTP_RP_BAD_SEGMENT = 2,
+       HTP_RP_BAD_INPUT = 3 };
+typedef struct {
+  int32_t batch, cap_points, cap_rows;  /* cap_points >= points of every path                  */
+  const int32_t* path_off;              /* [batch+1] CSR offsets into xs / ys / dirs           */
+  const double* xs;
+  const double* ys;
+  const double* dirs;                   /* +1 forward, -1 reverse                              */
+  const double* params;                 /* [batch][3]: WHEEL_BASE, desired_v, ds               */
+} htp_refpath_batch;
+typedef struct {
+  int32_t* status;                      /* [batch] HTP_RP_*                                    */
+  int32_t* n_rows;                      /* [batch]                                             */
+  double* traj;                         /* [batch][cap_rows][5] x, y, v, theta, steer          */
+} htp_refpath_result;
+int htp_init_ref_path_batch(htp_ctx* ctx, const htp_refpath_batch* in, htp_refpath_result* out);
+int htp_init_ref_path_batch_device(htp_ctx* ctx, const htp_refpath_batch* in, htp_refpath_result* out, void* stream);
+double htp_init_ref_path_last_ms(htp_ctx* ctx);
+
+/* ---------------------------------------------------------------------------
  * Reeds-Shepp: all admissible paths between pose pairs, sampled
  * (R/path_planner/utils/reeds_shepp.py calc_all_paths :39-65, called by
  * hybrid_a_star_search.py:248 and safety_forward_path_plan.py:368).

@@ -22,7 +22,8 @@ def build():
         return SO
     subprocess.check_call(["g++", "-O2", "-fno-builtin", "-std=c++17", "-shared", "-fPIC", "-o", SO,
                            os.path.join(CSRC, "htp_hostsim.cpp"), os.path.join(CSRC, "rs_hostsim.cpp"),
-                           os.path.join(CSRC, "hastar_hostsim.cpp"), os.path.join(CSRC, "ypark_hostsim.cpp")])
+                           os.path.join(CSRC, "hastar_hostsim.cpp"), os.path.join(CSRC, "ypark_hostsim.cpp"),
+                           os.path.join(CSRC, "refpath_hostsim.cpp")])
     return SO
 
 
@@ -37,6 +38,17 @@ def lib():
                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         _lib.htp_hostsim_obca_solve.restype = ctypes.c_int
     return _lib
+
+
+def init_ref_path_host(packed):
+    """refpath_core.h through the serial host build (same CSR batch as the GPU)."""
+    L = lib()
+    L.htp_hostsim_init_ref_path.argtypes = [ctypes.POINTER(_native.RpBatch), ctypes.POINTER(_native.RpResult)]
+    L.htp_hostsim_init_ref_path.restype = ctypes.c_int
+    res = _native.RefPathResults(packed)
+    b, r = packed.struct(), res.struct()
+    assert L.htp_hostsim_init_ref_path(ctypes.byref(b), ctypes.byref(r)) == 0
+    return res
 
 
 def solve_points(insts, options=None):

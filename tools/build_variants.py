@@ -28,7 +28,8 @@ for p in procs:
         sys.exit("build failed")
 for name in names:
     out = os.path.join(PKG, f"libhtp_{name}.so")
+    others = [os.path.join(OBJ, f) for f in sorted(os.listdir(OBJ))
+              if f.endswith(".hip.o") and f != "htp_obca.hip.o"]
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out,
-                           os.path.join(OBJ, f"htp_obca_{name}.o"), os.path.join(OBJ, "htp_rs.hip.o"),
-                           os.path.join(OBJ, "htp_hastar.hip.o")])
+                           os.path.join(OBJ, f"htp_obca_{name}.o")] + others)
     print("built", out)
