@@ -23,6 +23,15 @@
 #ifndef HTP_FI
 #define HTP_FI __attribute__((always_inline))
 #endif
+// IPM phases called from several sites (factorize, kkt_solve, line-search trial,
+// constraint / barrier / error evaluations): one out-of-line copy each keeps the
+// kernel's instruction footprint small (instruction-cache misses were a large
+// share of the per-iteration latency); helpers stay force-inlined.
+#ifdef HTP_OUTLINE_PHASES
+#define HTP_PHASE __attribute__((noinline))
+#else
+#define HTP_PHASE HTP_FI
+#endif
 
 namespace htp {
 
@@ -287,6 +296,15 @@ struct ObcaSolver {
   int n_factor;
   bool use_ric = false;
   long long cyc[8];
+#ifdef HTP_PROF_ON  // experiments: sub-step cycle counters of the stage chain (tools/build_variants.py)
+  long long pcyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tprof = 0;
+#define HTP_PROF(k) do { const long long t_ = c.clock(); pcyc[k] += t_ - tprof; tprof = t_; } while (0)
+#define HTP_PROF0() do { tprof = c.clock(); } while (0)
+#else
+#define HTP_PROF(k) do { } while (0)
+#define HTP_PROF0() do { } while (0)
+#endif
   // filter (wave-uniform): entries live in per-wave LDS (c.lds + FILT_OFF)
   static constexpr int FMAX = 64;
   static constexpr int FILT_OFF = 4 * NBMAX * NBMAX + 8;
@@ -379,13 +397,13 @@ struct ObcaSolver {
       for (int k = 0; k < NS; ++k) f += 5000.0 * sq(x[D.oS + k]);
     return f;
   }
-  HTP_HD HTP_FI double eval_f(const gd* x) const {
+  HTP_HD HTP_PHASE double eval_f(const gd* x) const {
     double f = 0.0;
     for (int i = c.lane; i < D.N; i += c.width) f += stage_obj(x, i);
     return c.sum(f);
   }
   // scaled gradient (sf * grad f) into g (all n entries written)
-  HTP_HD HTP_FI void eval_grad_f(const gd* x, gd* g, double scale) const {
+  HTP_HD HTP_PHASE void eval_grad_f(const gd* x, gd* g, double scale) const {
     const int N = D.N;
     const double dT = par(P_DT);
     const double Qs00 = 2 * par(P_Q00), Qs01 = par(P_Q01) + par(P_Q10), Qs11 = 2 * par(P_Q11);
@@ -524,7 +542,7 @@ struct ObcaSolver {
     out4[3] = c3;
   }
 
-  HTP_HD HTP_FI void eval_cons(const gd* x, gd* cc, gd* dd) const {
+  HTP_HD HTP_PHASE void eval_cons(const gd* x, gd* cc, gd* dd) const {
     const int N = D.N;
     const gd* scE = A(L.scE);
     const gd* scI = A(L.scI);
@@ -578,7 +596,7 @@ struct ObcaSolver {
   }
 
   // J_c' yc + J_d' yd (x part) into out (scaled rows; yc, yd multipliers of scaled rows)
-  HTP_HD HTP_FI void eval_jt(const gd* x, const gd* yc, const gd* yd, gd* out) {
+  HTP_HD HTP_PHASE void eval_jt(const gd* x, const gd* yc, const gd* yd, gd* out) {
     const int N = D.N;
     const gd* scE = A(L.scE);
     const gd* scI = A(L.scI);
@@ -1522,6 +1540,12 @@ struct ObcaSolver {
         add(NS + k, NS + k, st * st / Et);
       }
     }
+    // Riccati records: reciprocal scaling of this stage's multiplier rows
+    {
+      gd* Ss = A(L.LD) + (int64_t)i * nb * nb + SOFF;
+      const int yb = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
+      for (int k = 0; k < NS; ++k) Ss[k] = 1.0 / scE[yb + k];
+    }
     // off-diagonal block for i+1 (rows of block i+1, cols of block i)
     if (i < N - 1) {
       gd* O = A(L.Off) + (int64_t)(i + 1) * nb * nb;
@@ -1529,9 +1553,11 @@ struct ObcaSolver {
       double w[8], J[40];
       stage_w(x, i, w);
       dynJ(w, J);
+      gd* Js = A(L.LD) + (int64_t)i * nb * nb + JOFF;  // unscaled J_i (stride 8) for the Riccati records
       for (int k = 0; k < NS; ++k) {
         const double s_ = scE[D.eDyn + NS * i + k];
         for (int j = 0; j < D.nw; ++j) O[k * nb + NS + j] = -s_ * J[k * D.nw + j];
+        for (int j = 0; j < 8; ++j) Js[k * 8 + j] = (j < D.nw) ? J[k * D.nw + j] : 0.0;
       }
       if (PT && !ls && i < N - 2) {
         const int U0 = NS + 5;
@@ -1757,30 +1783,52 @@ struct ObcaSolver {
   // The block-tridiagonal KKT system has IPOPT's inertia iff every Rt is
   // positive definite (Rt are the pivot blocks of the reduced Hessian).
   // Per-stage storage (slot i of L.LD): P_i [0,64), K_i [64,88).
-  HTP_HD HTP_FI static bool chol3(const double* R, int nv, double* Lc) {  // Lc: 3x3 lower
+  // Cholesky of the leading nv x nv (nv <= 3) block of R (stride 3).  Lc holds
+  // the lower factor with the RECIPROCAL of each pivot on its diagonal, so the
+  // solves multiply instead of divide.  Loops run to 3 with `j < nv` guards:
+  // static register indices (no dynamic-index select chains).
+  HTP_HD HTP_FI static bool chol3(const double* R, int nv, double* Lc) {
     for (int k = 0; k < 9; ++k) Lc[k] = 0.0;
-    for (int j = 0; j < nv; ++j) {
-      double d = R[j * 3 + j];
-      for (int k = 0; k < j; ++k) d -= Lc[j * 3 + k] * Lc[j * 3 + k];
-      if (!(d > 0.0)) return false;
-      d = sqrt(d);
-      Lc[j * 3 + j] = d;
-      for (int r = j + 1; r < nv; ++r) {
-        double v = R[r * 3 + j];
-        for (int k = 0; k < j; ++k) v -= Lc[r * 3 + k] * Lc[j * 3 + k];
-        Lc[r * 3 + j] = v / d;
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j < nv) {
+        double d = R[j * 3 + j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) d -= Lc[j * 3 + k] * Lc[j * 3 + k];
+        if (!(d > 0.0)) ok = false;
+        const double id = 1.0 / sqrt(d);
+        Lc[j * 3 + j] = id;
+#pragma unroll
+        for (int r = j + 1; r < 3; ++r) {
+          if (r < nv) {
+            double v = R[r * 3 + j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) v -= Lc[r * 3 + k] * Lc[j * 3 + k];
+            Lc[r * 3 + j] = v * id;
+          }
+        }
       }
     }
-    return true;
+    return ok;
   }
   HTP_HD HTP_FI static void chol3_solve(const double* Lc, int nv, double* b) {
-    for (int j = 0; j < nv; ++j) {
-      for (int k = 0; k < j; ++k) b[j] -= Lc[j * 3 + k] * b[k];
-      b[j] /= Lc[j * 3 + j];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j < nv) {
+#pragma unroll
+        for (int k = 0; k < j; ++k) b[j] -= Lc[j * 3 + k] * b[k];
+        b[j] *= Lc[j * 3 + j];
+      }
     }
-    for (int j = nv - 1; j >= 0; --j) {
-      for (int k = j + 1; k < nv; ++k) b[j] -= Lc[k * 3 + j] * b[k];
-      b[j] /= Lc[j * 3 + j];
+#pragma unroll
+    for (int j = 2; j >= 0; --j) {
+      if (j < nv) {
+#pragma unroll
+        for (int k = j + 1; k < 3; ++k)
+          if (k < nv) b[j] -= Lc[k * 3 + j] * b[k];
+        b[j] *= Lc[j * 3 + j];
+      }
     }
   }
 
@@ -1819,10 +1867,7 @@ struct ObcaSolver {
         const int r = e / 8, q = e % 8;
         return (r < D.nw && q < D.nw) ? A(L.Kst)[(int64_t)i * nb * nb + (NS + r) * nb + NS + q] : 0.0;
       }
-      if (e < 104) {
-        const int k = (e - 64) / 8, j = (e - 64) % 8;
-        return (j < D.nw) ? -A(L.Off)[(int64_t)(i + 1) * nb * nb + k * nb + NS + j] / scE[D.eDyn + NS * i + k] : 0.0;
-      }
+      if (e < 104) return A(L.LD)[(int64_t)i * nb * nb + JOFF + (e - 64)];  // J_i, unscaled, stride 8
       if (e < 110) {
         const int a = (e - 104) / 3, b = (e - 104) % 3;
         return (i >= 1 && b < nv) ? A(L.Off)[(int64_t)i * nb * nb + (NS + 5 + a) * nb + NS + 5 + b] : 0.0;
@@ -1834,6 +1879,7 @@ struct ObcaSolver {
       for (int e = c.lane; e < 112; e += c.width) fb0[e] = rec(N - 2, e);
     c.sync();
     for (int i = N - 2; i >= 0; --i) {
+      HTP_PROF0();
       ld* cur = ((N - 2 - i) & 1) ? fb1 : fb0;
       ld* nxt = ((N - 2 - i) & 1) ? fb0 : fb1;
       double pre[PF];
@@ -1850,6 +1896,7 @@ struct ObcaSolver {
           if (e < 112) nxt[e] = pre[u];
         }
       c.sync();
+      HTP_PROF(0);
       // PJx = P[:,0:5] Jx ; PB = P[:,0:5] Jv + P[:,5:5+nv]
       for (int e = c.lane; e < nz * (NS + nv); e += c.width) {
         const int r = e / (NS + nv), q = e % (NS + nv);
@@ -1859,6 +1906,7 @@ struct ObcaSolver {
         else PB[r * 3 + (q - NS)] = acc + Pc[r * 8 + NS + (q - NS)];
       }
       c.sync();
+      HTP_PROF(1);
       // Rt = R + B'PB ; St = S + B'PA ; AtPA = Jx' P Jx
       for (int e = c.lane; e < nv * nv + nv * nz + 25; e += c.width) {
         if (e < nv * nv) {
@@ -1884,6 +1932,7 @@ struct ObcaSolver {
         }
       }
       c.sync();
+      HTP_PROF(2);
       // Cholesky of Rt (redundantly per lane) ; K = -Rt^-1 St (lane per column)
       double Rl[9], Lc[9];
       for (int k = 0; k < 9; ++k) Rl[k] = (k / 3 < nv && k % 3 < nv) ? Rt[k] : 0.0;
@@ -1891,11 +1940,16 @@ struct ObcaSolver {
       if (!pd) ++bad;
       for (int q = c.lane; q < nz; q += c.width) {
         double col[3] = {0.0, 0.0, 0.0};
-        for (int a = 0; a < nv; ++a) col[a] = St[a * 8 + q];
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+          if (a < nv) col[a] = St[a * 8 + q];
         if (pd) chol3_solve(Lc, nv, col);
-        for (int a = 0; a < nv; ++a) Kl[a * 8 + q] = -col[a];
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+          if (a < nv) Kl[a * 8 + q] = -col[a];
       }
       c.sync();
+      HTP_PROF(3);
       // P_i = Q + A'PA + St'K
       gd* Ps = A(L.LD) + (int64_t)i * nb * nb;
       for (int e = c.lane; e < 64; e += c.width) {
@@ -1913,6 +1967,7 @@ struct ObcaSolver {
       c.sync();
       for (int e = c.lane; e < 64; e += c.width) Pc[e] = 0.5 * (Pn[e] + Pn[(e % 8) * 8 + e / 8]);  // symmetrise
       c.sync();
+      HTP_PROF(5);
     }
     return bad;
   }
@@ -1922,50 +1977,57 @@ struct ObcaSolver {
   // wave loads with one coalesced round trip, one stage ahead of use
   // (double-buffered in LDS), so the sequential passes are LDS-latency bound.
   static constexpr int RB = 128;  // backward record
+  // per-stage slot of L.LD (nb*nb >= 144 doubles) on the Riccati path: P [0,64), K [64,88),
+  // chol(Rt) [88,97), unscaled dynamics Jacobian J_i [97,137), 1/scaling of the y_i rows [137,142)
+  static constexpr int JOFF = 97;
+  static constexpr int SOFF = 137;
   static constexpr int RF = 192;  // forward record
 
-  HTP_HD HTP_FI double rec_back(int i, int e, const gd* V) const {
-    const int nb = D.nb, nv = D.nw - NS, nz = NS + nv;
-    const gd* scE = A(L.scE);
-    if (e < 40) {  // P_{i+1}[r][t], r < 8, t < 5
-      const int r = e / 5, t = e % 5;
-      return (r < nz) ? A(L.LD)[(int64_t)(i + 1) * nb * nb + r * 8 + t] : 0.0;
-    }
-    if (e < 80) {  // J_i[k][j] (unscaled)
-      const int k = (e - 40) / 8, j = (e - 40) % 8;
-      return (j < D.nw) ? -A(L.Off)[(int64_t)(i + 1) * nb * nb + k * nb + NS + j] / scE[D.eDyn + NS * i + k] : 0.0;
-    }
-    if (e < 85) { const int k = e - 80; return V[(int64_t)(i + 1) * nb + k] / scE[D.eDyn + NS * i + k]; }
-    if (e < 90) return V[(int64_t)i * nb + NS + (e - 85)];
-    if (e < 93) return (e - 90 < nv) ? V[(int64_t)i * nb + NS + NS + (e - 90)] : 0.0;
-    if (e >= 96 && e < 120) return A(L.LD)[(int64_t)i * nb * nb + 64 + (e - 96)];
-    return 0.0;
+  // Record element e of stage i as (source, offset): the source pointer advances
+  // affinely with i, so the per-stage gather is one load (two for a scaled V
+  // entry) per element with no element-dependent branching.
+  enum { RK_ZERO = 0, RK_LDN, RK_LDC, RK_VNS, RK_VC, RK_XC };
+  struct RecDesc {
+    int kind, off, off2;
+    bool next;  // needs stage i + 1 (zero on the last stage)
+  };
+  HTP_HD HTP_FI RecDesc rec_back_desc(int e) const {
+    const int nv = D.nw - NS, nz = NS + nv;
+    const RecDesc z{RK_ZERO, 0, 0, false};
+    if (e < 40) { const int r = e / 5, t = e % 5; return (r < nz) ? RecDesc{RK_LDN, r * 8 + t, 0, false} : z; }  // P_{i+1}
+    if (e < 80) return (((e - 40) % 8) < D.nw) ? RecDesc{RK_LDC, JOFF + (e - 40), 0, false} : z;              // J_i
+    if (e < 85) return RecDesc{RK_VNS, e - 80, SOFF + (e - 80), false};                                        // e_{i+1}
+    if (e < 90) return RecDesc{RK_VC, NS + (e - 85), 0, false};                                                // q_i
+    if (e < 93) return (e - 90 < nv) ? RecDesc{RK_VC, NS + NS + (e - 90), 0, false} : z;                       // r_i
+    if (e >= 96 && e < 120) return RecDesc{RK_LDC, 64 + (e - 96), 0, false};                                   // K_i
+    return z;
   }
-
-  HTP_HD HTP_FI double rec_fwd(int i, int e, const gd* V, const gd* X) const {
-    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
-    const gd* scE = A(L.scE);
-    const int64_t slot = (int64_t)i * nb * nb;
-    if (e < 40) return A(L.LD)[slot + (e / 8) * 8 + (e % 8)];          // P_i rows 0..4
-    if (e < 48) return (e - 40 < nz) ? X[(int64_t)i * nb + (e - 40)] : 0.0;  // p_i
-    if (e < 51) return (i < N - 1 && e - 48 < nv) ? X[(int64_t)i * nb + nz + (e - 48)] : 0.0;  // rt_i
-    if (e < 60) return (i < N - 1) ? A(L.LD)[slot + 88 + (e - 51)] : 0.0;  // chol(Rt_i)
-    if (e < 84) return (i < N - 1) ? A(L.LD)[slot + 64 + (e - 60)] : 0.0;  // K_i
-    if (e < 124) {                                                       // J_i
-      if (i >= N - 1) return 0.0;
-      const int k = (e - 84) / 8, j = (e - 84) % 8;
-      return (j < D.nw) ? -A(L.Off)[(int64_t)(i + 1) * nb * nb + k * nb + NS + j] / scE[D.eDyn + NS * i + k] : 0.0;
-    }
-    if (e < 129) {                                                       // e_{i+1}
-      if (i >= N - 1) return 0.0;
-      const int k = e - 124;
-      return V[(int64_t)(i + 1) * nb + k] / scE[D.eDyn + NS * i + k];
-    }
-    if (e < 134) {                                                       // 1/sc of y_i rows
-      const int ybase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
-      return 1.0 / scE[ybase + (e - 129)];
-    }
-    return 0.0;
+  HTP_HD HTP_FI RecDesc rec_fwd_desc(int e) const {
+    const int nv = D.nw - NS, nz = NS + nv;
+    const RecDesc z{RK_ZERO, 0, 0, false};
+    if (e < 40) return RecDesc{RK_LDC, e, 0, false};                                                  // P_i rows 0..4
+    if (e < 48) return (e - 40 < nz) ? RecDesc{RK_XC, e - 40, 0, false} : z;                          // p_i
+    if (e < 51) return (e - 48 < nv) ? RecDesc{RK_XC, nz + (e - 48), 0, true} : z;                    // rt_i
+    if (e < 60) return RecDesc{RK_LDC, 88 + (e - 51), 0, true};                                      // chol(Rt_i)
+    if (e < 84) return RecDesc{RK_LDC, 64 + (e - 60), 0, true};                                      // K_i
+    if (e < 124) return (((e - 84) % 8) < D.nw) ? RecDesc{RK_LDC, JOFF + (e - 84), 0, true} : z;     // J_i
+    if (e < 129) return RecDesc{RK_VNS, e - 124, SOFF + (e - 124), true};                            // e_{i+1}
+    if (e < 134) return RecDesc{RK_LDC, SOFF + (e - 129), 0, false};                                 // 1/sc of y_i
+    return z;
+  }
+  HTP_HD HTP_FI double rec_get(const RecDesc& d, int i, const gd* V, const gd* X) const {
+    const int nb = D.nb;
+    const int64_t nb2 = (int64_t)nb * nb;
+    if (d.kind == RK_ZERO || (d.next && i >= D.N - 1)) return 0.0;
+    const gd* LDc = A(L.LD) + (int64_t)i * nb2;
+    const gd* src = (d.kind == RK_LDN) ? LDc + nb2
+                  : (d.kind == RK_LDC) ? LDc
+                  : (d.kind == RK_VNS) ? V + (int64_t)(i + 1) * nb
+                  : (d.kind == RK_VC) ? V + (int64_t)i * nb
+                                      : X + (int64_t)i * nb;
+    double v = src[d.off];
+    if (d.kind == RK_VNS) v *= LDc[nb2 + d.off2];
+    return v;
   }
 
   HTP_HD HTP_FI void riccati_solve(const gd* V, gd* X) {
@@ -1979,6 +2041,12 @@ struct ObcaSolver {
     ld* vv = pv + 32;             // v (3)
     ld* yv = pv + 40;             // y (5)
     constexpr int PB = (RF + Ctx::width - 1) / Ctx::width;
+    RecDesc db[PB], dfw[PB];
+#pragma unroll
+    for (int u = 0; u < PB; ++u) {
+      db[u] = rec_back_desc(c.lane + u * c.width);
+      dfw[u] = rec_fwd_desc(c.lane + u * c.width);
+    }
     // ---------------- backward: p_{N-1} = [q_{N-1}; 0]
     for (int k = c.lane; k < 8; k += c.width) {
       const double val = (k < NS) ? V[(int64_t)(N - 1) * nb + NS + k] : 0.0;
@@ -1986,15 +2054,17 @@ struct ObcaSolver {
       X[(int64_t)(N - 1) * nb + k] = val;
     }
     if (N >= 2)
-      for (int e = c.lane; e < RB; e += c.width) buf0[e] = rec_back(N - 2, e, V);
+      for (int u = 0; u < PB; ++u)
+        if (c.lane + u * c.width < RB) buf0[c.lane + u * c.width] = rec_get(db[u], N - 2, V, X);
     c.sync();
+    HTP_PROF0();
     for (int i = N - 2; i >= 0; --i) {
       ld* cur = ((N - 2 - i) & 1) ? buf1 : buf0;
       ld* nxt = ((N - 2 - i) & 1) ? buf0 : buf1;
       double pre[PB];
       for (int u = 0; u < PB; ++u) {
         const int e = c.lane + u * c.width;
-        pre[u] = (i > 0 && e < RB) ? rec_back(i - 1, e, V) : 0.0;
+        pre[u] = (i > 0 && e < RB) ? rec_get(db[u], i - 1, V, X) : 0.0;
       }
       for (int r = c.lane; r < nz; r += c.width) {  // w = p - P e
         double acc = pv[r];
@@ -2009,18 +2079,25 @@ struct ObcaSolver {
       }
       c.sync();
       gd* Xi = X + (int64_t)i * nb;
-      double pnew[8];
-      for (int r = c.lane; r < nz; r += c.width) {  // p = q + Jx' w + K' rt
-        double acc = (r < NS) ? cur[85 + r] : 0.0;
-        if (r < NS)
-          for (int t = 0; t < NS; ++t) acc += cur[40 + t * 8 + r] * wv[t];
-        for (int a2 = 0; a2 < nv; ++a2) acc += cur[96 + a2 * 8 + r] * rt[a2];
-        pnew[(r - c.lane) / c.width] = acc;
-        Xi[r] = acc;
+      constexpr int PN = (8 + Ctx::width - 1) / Ctx::width;
+      double pnew[PN];
+      {
+        int u = 0;
+        for (int r = c.lane; r < nz; r += c.width, ++u) {  // p = q + Jx' w + K' rt
+          double acc = (r < NS) ? cur[85 + r] : 0.0;
+          if (r < NS)
+            for (int t = 0; t < NS; ++t) acc += cur[40 + t * 8 + r] * wv[t];
+          for (int a2 = 0; a2 < nv; ++a2) acc += cur[96 + a2 * 8 + r] * rt[a2];
+          pnew[u] = acc;
+          Xi[r] = acc;
+        }
       }
       for (int a2 = c.lane; a2 < nv; a2 += c.width) Xi[nz + a2] = rt[a2];
       c.sync();
-      for (int r = c.lane; r < nz; r += c.width) pv[r] = pnew[(r - c.lane) / c.width];
+      {
+        int u = 0;
+        for (int r = c.lane; r < nz; r += c.width, ++u) pv[r] = pnew[u];
+      }
       if (i > 0)
         for (int u = 0; u < PB; ++u) {
           const int e = c.lane + u * c.width;
@@ -2028,12 +2105,14 @@ struct ObcaSolver {
         }
       c.sync();
     }
+    HTP_PROF(6);
     // ---------------- forward: z_0 = [x_0; 0]; v = Rt^-1 rt + K z; y = (p - P z)[0:5]
     {
       const gd* scE = A(L.scE);
       for (int k = c.lane; k < 8; k += c.width) zv[k] = (k < NS) ? V[k] / scE[k] : 0.0;
     }
-    for (int e = c.lane; e < RF; e += c.width) buf0[e] = rec_fwd(0, e, V, X);
+    for (int u = 0; u < PB; ++u)
+      if (c.lane + u * c.width < RF) buf0[c.lane + u * c.width] = rec_get(dfw[u], 0, V, X);
     c.sync();
     for (int i = 0; i < N; ++i) {
       ld* cur = (i & 1) ? buf1 : buf0;
@@ -2041,7 +2120,7 @@ struct ObcaSolver {
       double pre[PB];
       for (int u = 0; u < PB; ++u) {
         const int e = c.lane + u * c.width;
-        pre[u] = (i + 1 < N && e < RF) ? rec_fwd(i + 1, e, V, X) : 0.0;
+        pre[u] = (i + 1 < N && e < RF) ? rec_get(dfw[u], i + 1, V, X) : 0.0;
       }
       for (int k = c.lane; k < NS; k += c.width) {
         double acc = cur[40 + k];
@@ -2061,9 +2140,11 @@ struct ObcaSolver {
       }
       c.sync();
       gd* Xi = X + (int64_t)i * nb;
-      double zn[8];
+      constexpr int PN = (8 + Ctx::width - 1) / Ctx::width;
+      double zn[PN];
+      int un = 0;
       if (i < N - 1)
-        for (int k = c.lane; k < nz; k += c.width) {
+        for (int k = c.lane; k < nz; k += c.width, ++un) {
           double acc;
           if (k < NS) {
             acc = cur[124 + k];
@@ -2072,7 +2153,7 @@ struct ObcaSolver {
           } else {
             acc = vv[k - NS];
           }
-          zn[(k - c.lane) / c.width] = acc;
+          zn[un] = acc;
         }
       for (int k = c.lane; k < NS; k += c.width) {
         Xi[k] = yv[k];
@@ -2082,7 +2163,8 @@ struct ObcaSolver {
         for (int a2 = c.lane; a2 < nv; a2 += c.width) Xi[NS + NS + a2] = vv[a2];
       c.sync();
       if (i < N - 1) {
-        for (int k = c.lane; k < nz; k += c.width) zv[k] = zn[(k - c.lane) / c.width];
+        un = 0;
+        for (int k = c.lane; k < nz; k += c.width, ++un) zv[k] = zn[un];
         for (int u = 0; u < PB; ++u) {
           const int e = c.lane + u * c.width;
           if (e < RF) nxt[e] = pre[u];
@@ -2090,11 +2172,12 @@ struct ObcaSolver {
       }
       c.sync();
     }
+    HTP_PROF(7);
   }
 
   // ---------------------------------------------------------- factorization
   // returns true if the inertia is the one IPOPT requires
-  HTP_HD HTP_FI void factorize(bool ls, double dw, double dc, int& neg_out, int& zero_out) {
+  HTP_HD HTP_PHASE void factorize(bool ls, double dw, double dc, int& neg_out, int& zero_out) {
     const int N = D.N, nb = D.nb;
     int neg = 0, zero = 0;
     long long t0 = c.clock();
@@ -2189,7 +2272,7 @@ struct ObcaSolver {
   }
 
   // solve K [ox; os; oc; od] = [bx; bs; bc; bd] with the current factorization
-  HTP_HD HTP_FI void kkt_solve(bool ls, double dw, double dc, const gd* bx, const gd* bs, const gd* bc,
+  HTP_HD HTP_PHASE void kkt_solve(bool ls, double dw, double dc, const gd* bx, const gd* bs, const gd* bc,
                         const gd* bd, gd* ox, gd* os, gd* oc, gd* od) {
     const int N = D.N, nb = D.nb;
     const long long t0 = c.clock();
@@ -2328,7 +2411,7 @@ struct ObcaSolver {
     c.sync();
   }
 
-  HTP_HD HTP_FI Err errors(const gd* gl, double mu_) const {
+  HTP_HD HTP_PHASE Err errors(const gd* gl, double mu_) const {
     const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
     const gd* zL = A(L.zL); const gd* zU = A(L.zU);
     const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
@@ -2401,7 +2484,7 @@ struct ObcaSolver {
   }
 
   // barrier function; returns +inf (as 1e308*10) if a slack is not positive
-  HTP_HD HTP_FI double barrier(const gd* x, const gd* s, double mu_) const {
+  HTP_HD HTP_PHASE double barrier(const gd* x, const gd* s, double mu_) const {
     const gd* xL = A(L.xL); const gd* xU = A(L.xU);
     const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     const double kd = o.kappa_d * mu_;
@@ -2527,7 +2610,7 @@ struct ObcaSolver {
   }
 
   // trial acceptability test (filter / Armijo); evaluates ct, dt at (xt, st)
-  HTP_HD HTP_FI bool acceptable(double a, const gd* xt, const gd* st, double phi, double theta, double gBD,
+  HTP_HD HTP_PHASE bool acceptable(double a, const gd* xt, const gd* st, double phi, double theta, double gBD,
                          bool ftype_ok, double& th_t, double& ph_t) {
     gd* ct = A(L.ct);
     gd* dtv = A(L.dt);
@@ -2551,6 +2634,10 @@ struct ObcaSolver {
     iterate(res);
     if (c.lane == 0) {
       for (int k = 0; k < 8; ++k) res.cyc[k] = cyc[k];
+#ifdef HTP_PROF_ON
+      for (int k = 0; k < 8; ++k)
+        if (k != 4) res.cyc[k] = pcyc[k];
+#endif
       res.cyc[4] = c.clock() - t0;
     }
   }
