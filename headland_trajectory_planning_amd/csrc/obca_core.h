@@ -19,7 +19,12 @@
 #include "htp_common.h"
 #include "dyn_gen.h"
 
-#define HTP_UNROLL _Pragma("unroll 4")
+#ifndef HTP_UNROLL_N
+#define HTP_UNROLL_N 4
+#endif
+#define HTP_PRAGMA_(x) _Pragma(#x)
+#define HTP_PRAGMA(x) HTP_PRAGMA_(x)
+#define HTP_UNROLL HTP_PRAGMA(unroll HTP_UNROLL_N)
 #ifndef HTP_FI
 #define HTP_FI __attribute__((always_inline))
 #endif

@@ -47,14 +47,16 @@ def _kkt_residuals(nlp, x):
     return viol.max(), bnd.max()
 
 
-@pytest.mark.parametrize("cfg", ["B", "C"])
+@pytest.mark.parametrize("cfg", ["B", "C", "E"])
 def test_full_config_properties(ctx, cfg):
     _, N, M, imp = synth.CONFIGS[cfg]
-    insts = [synth.make_instance(pid, N=N, M=M, implement=imp) for pid in range(64)]
+    insts = [synth.make_instance(pid, N=N, M=M, implement=imp) for pid in range(64 if cfg != "E" else 16)]
     pk = _native.PackedBatch(insts)
     res = ctx.solve(pk)
     ok = np.isin(res.status, [0, 1])
-    assert ok.mean() >= 0.9, np.bincount(res.status)
+    # the rest are line-search failures where IPOPT would enter its restoration phase (not restated);
+    # the long-horizon pruner config E has more of them
+    assert ok.mean() >= (0.9 if cfg != "E" else 0.75), np.bincount(res.status)
     for k in np.where(ok)[0][:8]:
         nlp = ObcaNLP(insts[k])
         cv, bv = _kkt_residuals(nlp, res.x[k])
