@@ -113,8 +113,14 @@ struct LocalBlock {
       if (dk == 0.0) { zero = 1; dk = 1.0; }
       if (dk < 0.0) ++neg;
       K[pk(k, k)] = dk;
-      for (int r = k + 1; r < NL; ++r) K[pk(r, k)] = K[pk(r, k)] / dk;
+      const double idk = 1.0 / dk;  // one division per pivot, the column is scaled by multiplication
+      for (int r = k + 1; r < NL; ++r) K[pk(r, k)] = K[pk(r, k)] * idk;
     }
+  }
+  // W = L^-1 v (unit lower forward substitution only), in place
+  HTP_HD HTP_FI void forward(double* v) const {
+    for (int k = 0; k < NL; ++k)
+      for (int j = 0; j < k; ++j) v[k] -= K[pk(k, j)] * v[j];
   }
   HTP_HD HTP_FI void solve(double* v) const {  // in place K^-1 v
     for (int k = 0; k < NL; ++k)
@@ -1063,19 +1069,31 @@ struct ObcaSolver {
       neg += bneg;
       zero |= bzero;
       double S[6] = {0, 0, 0, 0, 0, 0};
-      for (int col = 0; col < 3; ++col) {
-        double v[NL];
-        for (int r = 0; r < NL; ++r) v[r] = B.B[r][col];
-        if (B.piv) for (int r = 0; r < NL; ++r) v[r] = Vp[col * NL + r];
-        else B.solve(v);
-        // S(:,col) = B' v
-        for (int row = 0; row <= col; ++row) {
-          double acc = 0.0;
-          for (int r = 0; r < NL; ++r) acc += B.B[r][row] * v[r];
-          // index map (row,col) -> xx0 xy1 yy2 xt3 yt4 tt5
-          const int idx = (col == 0) ? 0 : (col == 1 ? (row == 0 ? 1 : 2) : (row == 0 ? 3 : (row == 1 ? 4 : 5)));
-          S[idx] = acc;
+      if (B.piv) {
+        for (int col = 0; col < 3; ++col)
+          for (int row = 0; row <= col; ++row) {  // S(:,col) = B' K^-1 B(:,col)
+            double acc = 0.0;
+            for (int r = 0; r < NL; ++r) acc += B.B[r][row] * Vp[col * NL + r];
+            const int idx = (col == 0) ? 0 : (col == 1 ? (row == 0 ? 1 : 2) : (row == 0 ? 3 : (row == 1 ? 4 : 5)));
+            S[idx] = acc;
+          }
+      } else {
+        // B' K^-1 B = W' D^-1 W with W = L^-1 B: forward substitutions only
+        double W[3][NL];
+        for (int col = 0; col < 3; ++col) {
+          for (int r = 0; r < NL; ++r) W[col][r] = B.B[r][col];
+          B.forward(W[col]);
         }
+        double id[NL];
+        for (int r = 0; r < NL; ++r) id[r] = 1.0 / B.K[B.pk(r, r)];
+        for (int col = 0; col < 3; ++col)
+          for (int row = 0; row <= col; ++row) {
+            double acc = 0.0;
+            for (int r = 0; r < NL; ++r) acc += W[row][r] * (W[col][r] * id[r]);
+            // index map (row,col) -> xx0 xy1 yy2 xt3 yt4 tt5
+            const int idx = (col == 0) ? 0 : (col == 1 ? (row == 0 ? 1 : 2) : (row == 0 ? 3 : (row == 1 ? 4 : 5)));
+            S[idx] = acc;
+          }
       }
       for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
     }
