@@ -86,6 +86,28 @@ class CarModel:
         dirs = np.ones((len(path), 1)) * motion_command[1]
         return np.hstack((path, ks, dirs))
 
+    def calculate_motion_path_new(self, init_pose, motion_dir, steer_dir, turning_radius, delta_yaw, step_size=0.1):
+        """car_model.py:236-269: a circular arc of radius max(R_min, turning_radius) sampled in closed form;
+        rows [x, y, yaw, k, dir], the init pose repeated as the first row (as the reference does)."""
+        turning_radius = max(1.0 / self.curvature, turning_radius)
+        steer_angle = math.atan(self.WHEEL_BASE / turning_radius) * steer_dir
+        arc_length = abs(delta_yaw * turning_radius)
+        num_steps = int(arc_length / step_size)
+        actual_step_size = arc_length / num_steps
+        yaw_step = motion_dir * actual_step_size / self.WHEEL_BASE * math.tan(steer_angle)
+        init_x, init_y = init_pose[0], init_pose[1]
+        init_yaw = angle_wrap(init_pose[-1])
+        yaws = angle_wrap(np.linspace(init_yaw, init_yaw + yaw_step * num_steps, num_steps + 1))
+        xs = init_x + turning_radius * (np.sin(yaws) - np.sin(init_yaw)) * steer_dir
+        ys = init_y - turning_radius * (np.cos(yaws) - np.cos(init_yaw)) * steer_dir
+        path = np.vstack([init_pose, np.vstack([xs, ys, yaws]).T])
+        curvature = 0
+        if abs(steer_angle) > 0.00001:
+            curvature = math.tan(steer_angle) / self.WHEEL_BASE
+        ks = np.ones((len(path), 1)) * curvature
+        dirs = np.ones((len(path), 1)) * motion_dir
+        return np.hstack((path, ks, dirs))
+
     def get_turn_radius(self, max_steer_angle=None):
         if max_steer_angle is None:
             return 1 / self.curvature

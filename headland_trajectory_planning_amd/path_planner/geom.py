@@ -48,6 +48,12 @@ class Polygon:
         self.vertices = v
         self.exterior = _Ring(v)
 
+    @property
+    def bounds(self):
+        """(minx, miny, maxx, maxy), as shapely's."""
+        lo, hi = self.vertices.min(axis=0), self.vertices.max(axis=0)
+        return (float(lo[0]), float(lo[1]), float(hi[0]), float(hi[1]))
+
     def __repr__(self):
         return f"Polygon({self.vertices.shape[0]} vertices)"
 
@@ -207,3 +213,40 @@ def union_contains(lanes, F):
             reach = max(reach, hi)
         ok[e] = reach >= 1.0
     return ok.reshape(F.shape[0], F.shape[1]).all(1)
+
+
+def point_convex_distance(C, x, y):
+    """Euclidean distance from (x, y) to the closed convex ring C (0 inside)."""
+    if convex_contains_point(C, x, y):
+        return 0.0
+    a, b = C, np.roll(C, -1, axis=0)
+    e = b - a
+    ee = np.maximum(np.einsum("kd,kd->k", e, e), 1e-300)
+    t = np.clip(((x - a[:, 0]) * e[:, 0] + (y - a[:, 1]) * e[:, 1]) / ee, 0.0, 1.0)
+    px, py = a[:, 0] + t * e[:, 0] - x, a[:, 1] + t * e[:, 1] - y
+    return float(np.sqrt(np.min(px * px + py * py)))
+
+
+def polyline_buffer_intersects(xy, d, Q):
+    """LineString(xy).buffer(d, cap_style=2 (flat), join_style=1 (round)) intersects the
+    convex ring Q (R/path_planner/safety_forward_path_plan.py:815-818).
+
+    With flat caps and round joins the buffer is the union of one rectangle per
+    segment (the segment swept +-d along its normal) and a disc of radius d at
+    every interior vertex, so it touches Q iff a rectangle does (separating
+    axes) or an interior vertex lies within d of Q.  GEOS draws the join arcs
+    as inscribed chords (quadrant_segs 16), so the two predicates can only
+    disagree inside a band d (1 - cos(pi/64)) ~ 3.6e-4 d wide."""
+    xy = np.asarray(xy, dtype=np.float64)[:, :2]
+    keep = np.ones(len(xy), dtype=bool)
+    keep[1:] = np.any(xy[1:] != xy[:-1], axis=1)  # GEOS drops repeated points
+    xy = xy[keep]
+    if len(xy) < 2:
+        return point_convex_distance(Q, xy[0, 0], xy[0, 1]) <= d
+    p0, p1 = xy[:-1], xy[1:]
+    t = p1 - p0
+    n = np.stack([-t[:, 1], t[:, 0]], axis=1) / np.linalg.norm(t, axis=1)[:, None] * d
+    rects = np.stack([p0 + n, p1 + n, p1 - n, p0 - n], axis=1)
+    if convex_intersects(rects, Q).any():
+        return True
+    return any(point_convex_distance(Q, x, y) <= d for x, y in xy[1:-1])
