@@ -25,6 +25,17 @@ constexpr int LDS_D = 4 * NBMAX * NBMAX + 8 + 2 * 64;
 #define HTP_WAVES_PER_EU 1
 #endif
 
+// Residency cap (experiment knob): HTP_WG_LDS_BYTES = LDS bytes claimed per problem
+// (workgroup), so at most floor(160 KB / that) solver waves share one CU.  The
+// kernel never touches the padding.  Unset or 0: no cap (4 waves per CU).
+inline unsigned lds_pad_bytes() {
+  const char* e = getenv("HTP_WG_LDS_BYTES");
+  const long want = e ? atol(e) : 0;
+  const long fixed = (long)sizeof(double) * LDS_D + (long)sizeof(int) * 2 * NBMAX;
+  if (want <= fixed) return 0;
+  return (unsigned)(want > 160 * 1024 ? 160 * 1024 - fixed : want - fixed);
+}
+
 template <int EN, int EM>
 __global__ __launch_bounds__(64, HTP_WAVES_PER_EU) void obca_solve_kernel(const Shape* __restrict__ shp, BatchView b,
                                                         double* __restrict__ ws_all, int64_t ws_stride,
@@ -197,12 +208,18 @@ int htp_obca_solve_batch_device(htp_ctx* ctx, const htp_obca_batch* in, htp_obca
   bool u44 = true;
   for (int m = 0; m < D.M; ++m) u44 = u44 && D.eo[m] == 4;
   for (int k = 0; k < D.K; ++k) u44 = u44 && D.eb[k] == 4;
-  if (u44)
-    hipLaunchKernelGGL((obca_solve_kernel<4, 4>), dim3(in->batch), dim3(64), 0, s, (const Shape*)ctx->shape, b,
+  const unsigned pad = lds_pad_bytes();
+  if (u44) {
+    if (pad) HIPCHK(hipFuncSetAttribute((const void*)obca_solve_kernel<4, 4>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad));
+    hipLaunchKernelGGL((obca_solve_kernel<4, 4>), dim3(in->batch), dim3(64), pad, s, (const Shape*)ctx->shape, b,
                        (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
-  else
-    hipLaunchKernelGGL((obca_solve_kernel<MAXE, MAXE>), dim3(in->batch), dim3(64), 0, s, (const Shape*)ctx->shape, b,
+  } else {
+    if (pad) HIPCHK(hipFuncSetAttribute((const void*)obca_solve_kernel<MAXE, MAXE>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad));
+    hipLaunchKernelGGL((obca_solve_kernel<MAXE, MAXE>), dim3(in->batch), dim3(64), pad, s, (const Shape*)ctx->shape, b,
                        (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1, s));
   hipLaunchKernelGGL(unpack_results, dim3((in->batch + 255) / 256), dim3(256), 0, s, (const Result*)ctx->scratch,
