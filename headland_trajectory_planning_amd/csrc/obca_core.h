@@ -22,6 +22,9 @@
 #ifndef HTP_UNROLL_N
 #define HTP_UNROLL_N 4
 #endif
+#ifndef HTP_SWEEP_U
+#define HTP_SWEEP_U 4
+#endif
 #define HTP_PRAGMA_(x) _Pragma(#x)
 #define HTP_PRAGMA(x) HTP_PRAGMA_(x)
 #define HTP_UNROLL HTP_PRAGMA(unroll HTP_UNROLL_N)
@@ -333,6 +336,23 @@ struct ObcaSolver {
   HTP_HD HTP_FI static const gd* gp(const double* p) { return (const gd*)p; }
   HTP_HD HTP_FI double par(int k) const { return gp(in.par)[k]; }
   HTP_HD HTP_FI double tauv(const gd* x, int i) const { return D.topt ? x[D.oTAU + i] : 1.0; }
+
+  // Lane-blocked sweep over [0, n): per trip a lane takes SW_U indices q_k = b + k*width.
+  // ld(q, k) gathers element q into register slot k with the index clamped into range,
+  // so all loads of a trip issue before any use (a plain unrolled loop puts a bound
+  // check, and the elementwise bound tests, between them and waits one memory round trip
+  // per element).  op(q, k) then consumes the in-range slots in ascending k -- the
+  // plain loop's per-lane order, so reductions are bit-identical.
+  static constexpr int SW_U = HTP_SWEEP_U;
+  template <class Ld, class Op>
+  HTP_HD HTP_FI void sweep(int n, Ld&& ld_, Op&& op_) const {
+    for (int b = c.lane; b < n; b += SW_U * c.width) {
+      HTP_PRAGMA(unroll)
+      for (int k = 0; k < SW_U; ++k) { const int q = b + k * c.width; ld_(q < n ? q : n - 1, k); }
+      HTP_PRAGMA(unroll)
+      for (int k = 0; k < SW_U; ++k) { const int q = b + k * c.width; if (q < n) op_(q, k); }
+    }
+  }
 
   // pair p -> (i, m, n) and variable offsets
   HTP_HD HTP_FI void pair_index(int p, int& i, int& m, int& n, int& mu0, int& la0) const {
@@ -2442,29 +2462,38 @@ struct ObcaSolver {
     const gd* yc = A(L.yc); const gd* yd = A(L.yd);
     const gd* cc = A(L.c); const gd* dd = A(L.d);
     double dual = 0, comp = 0, zsum = 0, ysum = 0, pb = 0, pn = 0;
-    HTP_UNROLL
-    for (int q = c.lane; q < D.n; q += c.width) {
-      dual = dmax(dual, dabs(gl[q] - zL[q] + zU[q]));
-      if (finite_(xL[q])) { comp = dmax(comp, dabs((x[q] - xL[q]) * zL[q] - mu_)); zsum += dabs(zL[q]); }
-      if (finite_(xU[q])) { comp = dmax(comp, dabs((xU[q] - x[q]) * zU[q] - mu_)); zsum += dabs(zU[q]); }
+    {
+      double g_[SW_U], zl_[SW_U], zu_[SW_U], x_[SW_U], xl_[SW_U], xu_[SW_U];
+      sweep(D.n, [&](int q, int k) { g_[k] = gl[q]; zl_[k] = zL[q]; zu_[k] = zU[q]; x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; },
+            [&](int, int k) {
+              dual = dmax(dual, dabs(g_[k] - zl_[k] + zu_[k]));
+              if (finite_(xl_[k])) { comp = dmax(comp, dabs((x_[k] - xl_[k]) * zl_[k] - mu_)); zsum += dabs(zl_[k]); }
+              if (finite_(xu_[k])) { comp = dmax(comp, dabs((xu_[k] - x_[k]) * zu_[k] - mu_)); zsum += dabs(zu_[k]); }
+            });
     }
-    HTP_UNROLL
-    for (int r = c.lane; r < D.md; r += c.width) {
-      dual = dmax(dual, dabs(-yd[r] - vL[r] + vU[r]));
-      comp = dmax(comp, dabs((s[r] - dL[r]) * vL[r] - mu_));
-      zsum += dabs(vL[r]);
-      if (finite_(dU[r])) { comp = dmax(comp, dabs((dU[r] - s[r]) * vU[r] - mu_)); zsum += dabs(vU[r]); }
-      ysum += dabs(yd[r]);
-      pb = dmax(pb, dabs(dd[r] - s[r]));
-      double v = dmax(0.0, dL[r] - dd[r]);
-      if (finite_(dU[r])) v = dmax(v, dd[r] - dU[r]);
-      pn = dmax(pn, v);
+    {
+      double yd_[SW_U], vl_[SW_U], vu_[SW_U], s_[SW_U], dl_[SW_U], du_[SW_U], d_[SW_U];
+      sweep(D.md, [&](int r, int k) { yd_[k] = yd[r]; vl_[k] = vL[r]; vu_[k] = vU[r]; s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = dU[r]; d_[k] = dd[r]; },
+            [&](int, int k) {
+              dual = dmax(dual, dabs(-yd_[k] - vl_[k] + vu_[k]));
+              comp = dmax(comp, dabs((s_[k] - dl_[k]) * vl_[k] - mu_));
+              zsum += dabs(vl_[k]);
+              if (finite_(du_[k])) { comp = dmax(comp, dabs((du_[k] - s_[k]) * vu_[k] - mu_)); zsum += dabs(vu_[k]); }
+              ysum += dabs(yd_[k]);
+              pb = dmax(pb, dabs(d_[k] - s_[k]));
+              double v = dmax(0.0, dl_[k] - d_[k]);
+              if (finite_(du_[k])) v = dmax(v, d_[k] - du_[k]);
+              pn = dmax(pn, v);
+            });
     }
-    HTP_UNROLL
-    for (int r = c.lane; r < D.mc; r += c.width) {
-      ysum += dabs(yc[r]);
-      pb = dmax(pb, dabs(cc[r]));
-      pn = dmax(pn, dabs(cc[r]));
+    {
+      double yc_[SW_U], c_[SW_U];
+      sweep(D.mc, [&](int r, int k) { yc_[k] = yc[r]; c_[k] = cc[r]; },
+            [&](int, int k) {
+              ysum += dabs(yc_[k]);
+              pb = dmax(pb, dabs(c_[k]));
+              pn = dmax(pn, dabs(c_[k]));
+            });
     }
     Err e;
     e.dual = c.maxv(dual);
@@ -2485,24 +2514,34 @@ struct ObcaSolver {
     const gd* scE = A(L.scE); const gd* scI = A(L.scI);
     const double dmn = par(P_DMIN);
     double v = 0;
-    HTP_UNROLL
-    for (int r = c.lane; r < D.mc; r += c.width) v = dmax(v, dabs(cc[r]) / scE[r]);
-    HTP_UNROLL
-    for (int r = c.lane; r < D.md; r += c.width) {
-      const double g = dd[r] / scI[r];
-      if ((r & 1) == 0) v = dmax(v, dmax(0.0 - g, g - 1.0));
-      else if (PT) v = dmax(v, dmax(dmn - g, g - 100000.0));
-      else v = dmax(v, dmn - g);
+    {
+      double c_[SW_U], e_[SW_U];
+      sweep(D.mc, [&](int r, int k) { c_[k] = cc[r]; e_[k] = scE[r]; },
+            [&](int, int k) { v = dmax(v, dabs(c_[k]) / e_[k]); });
+    }
+    {
+      double d_[SW_U], i_[SW_U];
+      sweep(D.md, [&](int r, int k) { d_[k] = dd[r]; i_[k] = scI[r]; },
+            [&](int r, int k) {
+              const double g = d_[k] / i_[k];
+              if ((r & 1) == 0) v = dmax(v, dmax(0.0 - g, g - 1.0));
+              else if (PT) v = dmax(v, dmax(dmn - g, g - 100000.0));
+              else v = dmax(v, dmn - g);
+            });
     }
     return c.maxv(v);
   }
 
   HTP_HD HTP_FI double theta_of(const gd* cc, const gd* dd, const gd* s) const {
     double t = 0;
-    HTP_UNROLL
-    for (int r = c.lane; r < D.mc; r += c.width) t += dabs(cc[r]);
-    HTP_UNROLL
-    for (int r = c.lane; r < D.md; r += c.width) t += dabs(dd[r] - s[r]);
+    {
+      double c_[SW_U];
+      sweep(D.mc, [&](int r, int k) { c_[k] = cc[r]; }, [&](int, int k) { t += dabs(c_[k]); });
+    }
+    {
+      double d_[SW_U], s_[SW_U];
+      sweep(D.md, [&](int r, int k) { d_[k] = dd[r]; s_[k] = s[r]; }, [&](int, int k) { t += dabs(d_[k] - s_[k]); });
+    }
     return c.sum(t);
   }
 
@@ -2513,19 +2552,25 @@ struct ObcaSolver {
     const double kd = o.kappa_d * mu_;
     double lg = 0.0, lin = 0.0;
     int bad = 0;
-    HTP_UNROLL
-    for (int q = c.lane; q < D.n; q += c.width) {
-      const bool hl = finite_(xL[q]), hu = finite_(xU[q]);
-      if (hl) { const double v = x[q] - xL[q]; if (v <= 0) bad = 1; else lg += log(v); if (!hu) lin += v; }
-      if (hu) { const double v = xU[q] - x[q]; if (v <= 0) bad = 1; else lg += log(v); if (!hl) lin += v; }
+    {
+      double x_[SW_U], xl_[SW_U], xu_[SW_U];
+      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; },
+            [&](int, int k) {
+              const bool hl = finite_(xl_[k]), hu = finite_(xu_[k]);
+              if (hl) { const double v = x_[k] - xl_[k]; if (v <= 0) bad = 1; else lg += log(v); if (!hu) lin += v; }
+              if (hu) { const double v = xu_[k] - x_[k]; if (v <= 0) bad = 1; else lg += log(v); if (!hl) lin += v; }
+            });
     }
-    HTP_UNROLL
-    for (int r = c.lane; r < D.md; r += c.width) {
-      const bool hu = finite_(dU[r]);
-      const double v = s[r] - dL[r];
-      if (v <= 0) bad = 1; else lg += log(v);
-      if (!hu) lin += v;
-      if (hu) { const double w = dU[r] - s[r]; if (w <= 0) bad = 1; else lg += log(w); }
+    {
+      double s_[SW_U], dl_[SW_U], du_[SW_U];
+      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = dU[r]; },
+            [&](int, int k) {
+              const bool hu = finite_(du_[k]);
+              const double v = s_[k] - dl_[k];
+              if (v <= 0) bad = 1; else lg += log(v);
+              if (!hu) lin += v;
+              if (hu) { const double w = du_[k] - s_[k]; if (w <= 0) bad = 1; else lg += log(w); }
+            });
     }
     bad = c.isum(bad);
     lg = c.sum(lg);
@@ -2540,23 +2585,29 @@ struct ObcaSolver {
     const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     const gd* gf = A(L.gf);
     const double kd = o.kappa_d * mu_;
-    HTP_UNROLL
-    for (int q = c.lane; q < D.n; q += c.width) {
-      const bool hl = finite_(xL[q]), hu = finite_(xU[q]);
-      double g = gf[q];
-      if (hl) g -= mu_ / (x[q] - xL[q]);
-      if (hu) g += mu_ / (xU[q] - x[q]);
-      if (hl && !hu) g += kd;
-      if (hu && !hl) g -= kd;
-      gx[q] = g;
+    {
+      double x_[SW_U], xl_[SW_U], xu_[SW_U], g_[SW_U];
+      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; g_[k] = gf[q]; },
+            [&](int q, int k) {
+              const bool hl = finite_(xl_[k]), hu = finite_(xu_[k]);
+              double g = g_[k];
+              if (hl) g -= mu_ / (x_[k] - xl_[k]);
+              if (hu) g += mu_ / (xu_[k] - x_[k]);
+              if (hl && !hu) g += kd;
+              if (hu && !hl) g -= kd;
+              gx[q] = g;
+            });
     }
-    HTP_UNROLL
-    for (int r = c.lane; r < D.md; r += c.width) {
-      const bool hu = finite_(dU[r]);
-      double g = -mu_ / (s[r] - dL[r]);
-      if (hu) g += mu_ / (dU[r] - s[r]);
-      else g += kd;
-      gs[r] = g;
+    {
+      double s_[SW_U], dl_[SW_U], du_[SW_U];
+      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = dU[r]; },
+            [&](int r, int k) {
+              const bool hu = finite_(du_[k]);
+              double g = -mu_ / (s_[k] - dl_[k]);
+              if (hu) g += mu_ / (du_[k] - s_[k]);
+              else g += kd;
+              gs[r] = g;
+            });
     }
     c.sync();
   }
@@ -2565,15 +2616,21 @@ struct ObcaSolver {
     const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
     const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     double a = 1.0;
-    HTP_UNROLL
-    for (int q = c.lane; q < D.n; q += c.width) {
-      if (finite_(xL[q]) && dx[q] < 0) a = dmin(a, -tau * (x[q] - xL[q]) / dx[q]);
-      if (finite_(xU[q]) && -dx[q] < 0) a = dmin(a, -tau * (xU[q] - x[q]) / (-dx[q]));
+    {
+      double x_[SW_U], xl_[SW_U], xu_[SW_U], d_[SW_U];
+      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; d_[k] = dx[q]; },
+            [&](int, int k) {
+              if (finite_(xl_[k]) && d_[k] < 0) a = dmin(a, -tau * (x_[k] - xl_[k]) / d_[k]);
+              if (finite_(xu_[k]) && -d_[k] < 0) a = dmin(a, -tau * (xu_[k] - x_[k]) / (-d_[k]));
+            });
     }
-    HTP_UNROLL
-    for (int r = c.lane; r < D.md; r += c.width) {
-      if (ds[r] < 0) a = dmin(a, -tau * (s[r] - dL[r]) / ds[r]);
-      if (finite_(dU[r]) && -ds[r] < 0) a = dmin(a, -tau * (dU[r] - s[r]) / (-ds[r]));
+    {
+      double s_[SW_U], dl_[SW_U], du_[SW_U], d_[SW_U];
+      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = dU[r]; d_[k] = ds[r]; },
+            [&](int, int k) {
+              if (d_[k] < 0) a = dmin(a, -tau * (s_[k] - dl_[k]) / d_[k]);
+              if (finite_(du_[k]) && -d_[k] < 0) a = dmin(a, -tau * (du_[k] - s_[k]) / (-d_[k]));
+            });
     }
     return c.minv(a);
   }
@@ -2586,23 +2643,29 @@ struct ObcaSolver {
     const gd* vL = A(L.vL); const gd* vU = A(L.vU);
     gd* dzL = A(L.dzL); gd* dzU = A(L.dzU); gd* dvL = A(L.dvL); gd* dvU = A(L.dvU);
     double a = 1.0;
-    HTP_UNROLL
-    for (int q = c.lane; q < D.n; q += c.width) {
-      double t = 0.0, u = 0.0;
-      if (finite_(xL[q])) { const double sl = x[q] - xL[q]; t = (mu - zL[q] * sl - zL[q] * dx[q]) / sl; if (t < 0) a = dmin(a, -tau * zL[q] / t); }
-      if (finite_(xU[q])) { const double su = xU[q] - x[q]; u = (mu - zU[q] * su + zU[q] * dx[q]) / su; if (u < 0) a = dmin(a, -tau * zU[q] / u); }
-      dzL[q] = t;
-      dzU[q] = u;
+    {
+      double x_[SW_U], xl_[SW_U], xu_[SW_U], zl_[SW_U], zu_[SW_U], d_[SW_U];
+      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; zl_[k] = zL[q]; zu_[k] = zU[q]; d_[k] = dx[q]; },
+            [&](int q, int k) {
+              double t = 0.0, u = 0.0;
+              if (finite_(xl_[k])) { const double sl = x_[k] - xl_[k]; t = (mu - zl_[k] * sl - zl_[k] * d_[k]) / sl; if (t < 0) a = dmin(a, -tau * zl_[k] / t); }
+              if (finite_(xu_[k])) { const double su = xu_[k] - x_[k]; u = (mu - zu_[k] * su + zu_[k] * d_[k]) / su; if (u < 0) a = dmin(a, -tau * zu_[k] / u); }
+              dzL[q] = t;
+              dzU[q] = u;
+            });
     }
-    HTP_UNROLL
-    for (int r = c.lane; r < D.md; r += c.width) {
-      const double sl = s[r] - dL[r];
-      const double t = (mu - vL[r] * sl - vL[r] * ds[r]) / sl;
-      if (t < 0) a = dmin(a, -tau * vL[r] / t);
-      double u = 0.0;
-      if (finite_(dU[r])) { const double su = dU[r] - s[r]; u = (mu - vU[r] * su + vU[r] * ds[r]) / su; if (u < 0) a = dmin(a, -tau * vU[r] / u); }
-      dvL[r] = t;
-      dvU[r] = u;
+    {
+      double s_[SW_U], dl_[SW_U], du_[SW_U], vl_[SW_U], vu_[SW_U], d_[SW_U];
+      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = dU[r]; vl_[k] = vL[r]; vu_[k] = vU[r]; d_[k] = ds[r]; },
+            [&](int r, int k) {
+              const double sl = s_[k] - dl_[k];
+              const double t = (mu - vl_[k] * sl - vl_[k] * d_[k]) / sl;
+              if (t < 0) a = dmin(a, -tau * vl_[k] / t);
+              double u = 0.0;
+              if (finite_(du_[k])) { const double su = du_[k] - s_[k]; u = (mu - vu_[k] * su + vu_[k] * d_[k]) / su; if (u < 0) a = dmin(a, -tau * vu_[k] / u); }
+              dvL[r] = t;
+              dvU[r] = u;
+            });
     }
     c.sync();
     return c.minv(a);
@@ -2927,21 +2990,34 @@ struct ObcaSolver {
         const gd* xL = A(L.xL); const gd* xU = A(L.xU);
         const gd* dL = A(L.dL); const gd* dU = A(L.dU);
         const double ks = o.kappa_sigma;
-        HTP_UNROLL
-        for (int q = c.lane; q < D.n; q += c.width) {
-          x[q] += a_primal * dx[q];
-          if (finite_(xL[q])) { const double z = zL[q] + a_dual * dzL[q], v = x[q] - xL[q]; zL[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
-          if (finite_(xU[q])) { const double z = zU[q] + a_dual * dzU[q], v = xU[q] - x[q]; zU[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+        {
+          double x_[SW_U], d_[SW_U], xl_[SW_U], xu_[SW_U], zl_[SW_U], zu_[SW_U], dzl_[SW_U], dzu_[SW_U];
+          sweep(D.n, [&](int q, int k) { x_[k] = x[q]; d_[k] = dx[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; zl_[k] = zL[q];
+                                          zu_[k] = zU[q]; dzl_[k] = dzL[q]; dzu_[k] = dzU[q]; },
+                [&](int q, int k) {
+                  const double xn = x_[k] + a_primal * d_[k];
+                  x[q] = xn;
+                  if (finite_(xl_[k])) { const double z = zl_[k] + a_dual * dzl_[k], v = xn - xl_[k]; zL[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+                  if (finite_(xu_[k])) { const double z = zu_[k] + a_dual * dzu_[k], v = xu_[k] - xn; zU[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+                });
         }
-        HTP_UNROLL
-        for (int r = c.lane; r < D.md; r += c.width) {
-          s[r] += a_primal * ds[r];
-          yd[r] += a_primal * dyd[r];
-          { const double z = vL[r] + a_dual * dvL[r], v = s[r] - dL[r]; vL[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
-          if (finite_(dU[r])) { const double z = vU[r] + a_dual * dvU[r], v = dU[r] - s[r]; vU[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+        {
+          double s_[SW_U], d_[SW_U], y_[SW_U], dy_[SW_U], vl_[SW_U], dvl_[SW_U], dl_[SW_U], vu_[SW_U], dvu_[SW_U], du_[SW_U];
+          sweep(D.md, [&](int r, int k) { s_[k] = s[r]; d_[k] = ds[r]; y_[k] = yd[r]; dy_[k] = dyd[r]; vl_[k] = vL[r];
+                                           dvl_[k] = dvL[r]; dl_[k] = dL[r]; vu_[k] = vU[r]; dvu_[k] = dvU[r]; du_[k] = dU[r]; },
+                [&](int r, int k) {
+                  const double sn = s_[k] + a_primal * d_[k];
+                  s[r] = sn;
+                  yd[r] = y_[k] + a_primal * dy_[k];
+                  { const double z = vl_[k] + a_dual * dvl_[k], v = sn - dl_[k]; vL[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+                  if (finite_(du_[k])) { const double z = vu_[k] + a_dual * dvu_[k], v = du_[k] - sn; vU[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+                });
         }
-        HTP_UNROLL
-        for (int r = c.lane; r < D.mc; r += c.width) yc[r] += a_primal * dyc[r];
+        {
+          double y_[SW_U], dy_[SW_U];
+          sweep(D.mc, [&](int r, int k) { y_[k] = yc[r]; dy_[k] = dyc[r]; },
+                [&](int r, int k) { yc[r] = y_[k] + a_primal * dy_[k]; });
+        }
         c.sync();
       }
       {  // constraint values at the new point = those of the accepted trial point
