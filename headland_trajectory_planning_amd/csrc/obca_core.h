@@ -498,12 +498,22 @@ struct ObcaSolver {
     pair_index(p, i, m, n, mu0, la0);
     const int em = D.eo[m];
     const gd* Am = gp(in.obsA) + 2 * D.offo[m];
-    w[0] = w[1] = 0.0;
-    for (int j = 0; j < em; ++j) {
-      w[0] += Am[2 * j] * x[la0 + j];
-      w[1] += Am[2 * j + 1] * x[la0 + j];
+    // loads first (indices clamped), then the em-term sums in the plain order
+    double a0[EM_], a1[EM_], lx[EM_];
+    for (int j = 0; j < EM_; ++j) {
+      const int jj = j < em ? j : 0;
+      a0[j] = Am[2 * jj];
+      a1[j] = Am[2 * jj + 1];
+      lx[j] = x[la0 + jj];
     }
     const double th = x[NS * i + 3];
+    w[0] = w[1] = 0.0;
+    for (int j = 0; j < EM_; ++j) {
+      if (j < em) {
+        w[0] += a0[j] * lx[j];
+        w[1] += a1[j] * lx[j];
+      }
+    }
     cs = cos(th);
     sn = sin(th);
   }
@@ -558,15 +568,28 @@ struct ObcaSolver {
     const gd* bm = gp(in.obsb) + D.offo[m];
     const gd* Gn = gp(in.bodyG) + 2 * D.offb[n];
     const gd* gn = gp(in.bodyg) + D.offb[n];
-    double c2a = cs * w[0] + sn * w[1], c2b = -sn * w[0] + cs * w[1], c3 = 0.0;
-    for (int j = 0; j < en; ++j) {
-      const double mu = x[mu0 + j];
-      c2a += Gn[2 * j] * mu;
-      c2b += Gn[2 * j + 1] * mu;
-      c3 -= gn[j] * mu;
+    // loads first (indices clamped), then the plain-order sums over the en / em live entries
+    double muj[EN_], g0[EN_], g1[EN_], gj[EN_];
+    for (int j = 0; j < EN_; ++j) {
+      const int jj = j < en ? j : 0;
+      muj[j] = x[mu0 + jj]; g0[j] = Gn[2 * jj]; g1[j] = Gn[2 * jj + 1]; gj[j] = gn[jj];
+    }
+    double a0[EM_], a1[EM_], bj[EM_], lj[EM_];
+    for (int j = 0; j < EM_; ++j) {
+      const int jj = j < em ? j : 0;
+      a0[j] = Am[2 * jj]; a1[j] = Am[2 * jj + 1]; bj[j] = bm[jj]; lj[j] = x[la0 + jj];
     }
     const double tx = x[NS * i], ty = x[NS * i + 1];
-    for (int j = 0; j < em; ++j) c3 += (Am[2 * j] * tx + Am[2 * j + 1] * ty - bm[j]) * x[la0 + j];
+    double c2a = cs * w[0] + sn * w[1], c2b = -sn * w[0] + cs * w[1], c3 = 0.0;
+    for (int j = 0; j < EN_; ++j) {
+      if (j < en) {
+        c2a += g0[j] * muj[j];
+        c2b += g1[j] * muj[j];
+        c3 -= gj[j] * muj[j];
+      }
+    }
+    for (int j = 0; j < EM_; ++j)
+      if (j < em) c3 += (a0[j] * tx + a1[j] * ty - bj[j]) * lj[j];
     out4[0] = w[0] * w[0] + w[1] * w[1];
     out4[1] = c2a;
     out4[2] = c2b;
@@ -940,6 +963,34 @@ struct ObcaSolver {
     constexpr int NZ = LocalBlock<EN, EM>::NZ;
     constexpr int NL = LocalBlock<EN, EM>::NL;
     const int re = D.ePair + 2 * p;
+    // every load of the block issues here, unconditionally (indices clamped into range)
+    const int r1 = 2 * p, r3 = 2 * p + 1;
+    const double vL1 = vL[r1], sv1 = s[r1], dL1 = dL[r1], vU1 = vU[r1], dU1 = dU[r1];
+    const double vL3 = vL[r3], sv3 = s[r3], dL3 = dL[r3];
+    double zq[NZ], xq[NZ], xlq[NZ];
+    for (int j = 0; j < NZ; ++j) {
+      const bool is_mu = j < EN;
+      const int jj = is_mu ? j : j - EN;
+      const bool on = is_mu ? (jj < en) : (jj < em);
+      const int vi = on ? (is_mu ? mu0 + jj : la0 + jj) : mu0;
+      zq[j] = zL[vi];
+      xq[j] = x[vi];
+      xlq[j] = xL[vi];
+    }
+    double Am0[EM], Am1[EM], bmj[EM];
+    for (int j = 0; j < EM; ++j) {
+      const int jj = j < em ? j : 0;
+      Am0[j] = Am[2 * jj];
+      Am1[j] = Am[2 * jj + 1];
+      bmj[j] = bm[jj];
+    }
+    double Gn0[EN], Gn1[EN], gnj[EN];
+    for (int j = 0; j < EN; ++j) {
+      const int jj = j < en ? j : 0;
+      Gn0[j] = Gn[2 * jj];
+      Gn1[j] = Gn[2 * jj + 1];
+      gnj[j] = gn[jj];
+    }
     const double sa = scE[re], sb = scE[re + 1], s1 = scI[2 * p], s3 = scI[2 * p + 1];
     const double ya = sa * yc[re], yb = sb * yc[re + 1], y1 = s1 * yd[2 * p], y3 = s3 * yd[2 * p + 1];
     const double tx = x[NS * i], ty = x[NS * i + 1];
@@ -948,9 +999,8 @@ struct ObcaSolver {
       B.Ds1 = 1.0;
       B.Ds3 = 1.0;
     } else {
-      const int r1 = 2 * p, r3 = 2 * p + 1;
-      B.Ds1 = vL[r1] / (s[r1] - dL[r1]) + vU[r1] / (dU[r1] - s[r1]) + dw;
-      B.Ds3 = vL[r3] / (s[r3] - dL[r3]) + dw;
+      B.Ds1 = vL1 / (sv1 - dL1) + vU1 / (dU1 - sv1) + dw;
+      B.Ds3 = vL3 / (sv3 - dL3) + dw;
     }
     B.E1 = 1.0 / B.Ds1 + dc;
     B.E3 = 1.0 / B.Ds3 + dc;
@@ -958,17 +1008,17 @@ struct ObcaSolver {
     double Aw[EM], Atb[EM], A0[EM], A1[EM];
     for (int j = 0; j < EM; ++j) {
       const bool on = j < em;
-      A0[j] = on ? Am[2 * j] : 0.0;
-      A1[j] = on ? Am[2 * j + 1] : 0.0;
+      A0[j] = on ? Am0[j] : 0.0;
+      A1[j] = on ? Am1[j] : 0.0;
       Aw[j] = A0[j] * w[0] + A1[j] * w[1];
-      Atb[j] = on ? A0[j] * tx + A1[j] * ty - bm[j] : 0.0;
+      Atb[j] = on ? A0[j] * tx + A1[j] * ty - bmj[j] : 0.0;
     }
     double G0[EN], G1[EN], gg[EN];
     for (int j = 0; j < EN; ++j) {
       const bool on = j < en;
-      G0[j] = on ? Gn[2 * j] : 0.0;
-      G1[j] = on ? Gn[2 * j + 1] : 0.0;
-      gg[j] = on ? gn[j] : 0.0;
+      G0[j] = on ? Gn0[j] : 0.0;
+      G1[j] = on ? Gn1[j] : 0.0;
+      gg[j] = on ? gnj[j] : 0.0;
     }
     for (int j = 0; j < EN; ++j) {
       B.J1[j] = 0.0;
@@ -999,8 +1049,7 @@ struct ObcaSolver {
       } else if (ls) {
         dg = 1.0;
       } else {
-        const int vi = is_mu ? mu0 + jj : la0 + jj;
-        dg = zL[vi] / (x[vi] - xL[vi]) + dw;
+        dg = zq[j] / (xq[j] - xlq[j]) + dw;
       }
       B.K[B.pk(j, j)] += dg;
     }
@@ -1129,22 +1178,28 @@ struct ObcaSolver {
     }
     gd* PR = A(L.pairR);
     for (int p = c.lane; p < D.P; p += c.width) {
-      LocalBlock<EN, EM> B;
-      build_local<EN, EM>(B, p, ls, dw, dc);
-      B.factor();
       constexpr int NZ = LocalBlock<EN, EM>::NZ;
       constexpr int NL = LocalBlock<EN, EM>::NL;
       int i, m, n, mu0, la0;
       pair_index(p, i, m, n, mu0, la0);
       const int em = D.eo[m], en = D.eb[n];
-      const double q1 = (bd[2 * p] + bs[2 * p] / B.Ds1) / B.E1;
-      const double q3 = (bd[2 * p + 1] + bs[2 * p + 1] / B.Ds3) / B.E3;
-      double v[NL];
-      for (int j = 0; j < EN; ++j) v[j] = (j < en ? bx[mu0 + j] : 0.0) + B.J1[j] * q1 + B.J3z[j] * q3;
-      for (int j = 0; j < EM; ++j) v[EN + j] = (j < em ? bx[la0 + j] : 0.0) + B.J1[EN + j] * q1 + B.J3z[EN + j] * q3;
       const int re = D.ePair + 2 * p;
-      v[NZ] = bc[re];
-      v[NZ + 1] = bc[re + 1];
+      // rhs loads issue with the block's own loads (before its factorization)
+      const double bd1 = bd[2 * p], bs1 = bs[2 * p], bd3 = bd[2 * p + 1], bs3 = bs[2 * p + 1];
+      const double bc0 = bc[re], bc1 = bc[re + 1];
+      double bxz[NZ];
+      for (int j = 0; j < EN; ++j) bxz[j] = bx[mu0 + (j < en ? j : 0)];
+      for (int j = 0; j < EM; ++j) bxz[EN + j] = bx[la0 + (j < em ? j : 0)];
+      LocalBlock<EN, EM> B;
+      build_local<EN, EM>(B, p, ls, dw, dc);
+      B.factor();
+      const double q1 = (bd1 + bs1 / B.Ds1) / B.E1;
+      const double q3 = (bd3 + bs3 / B.Ds3) / B.E3;
+      double v[NL];
+      for (int j = 0; j < EN; ++j) v[j] = (j < en ? bxz[j] : 0.0) + B.J1[j] * q1 + B.J3z[j] * q3;
+      for (int j = 0; j < EM; ++j) v[EN + j] = (j < em ? bxz[EN + j] : 0.0) + B.J1[EN + j] * q1 + B.J3z[EN + j] * q3;
+      v[NZ] = bc0;
+      v[NZ + 1] = bc1;
       if (B.piv) {
         double vp[NL];
         int pn[2];
@@ -1171,23 +1226,29 @@ struct ObcaSolver {
       return;
     }
     for (int p = c.lane; p < D.P; p += c.width) {
-      LocalBlock<EN, EM> B;
-      build_local<EN, EM>(B, p, ls, dw, dc);
-      B.factor();
       constexpr int NZ = LocalBlock<EN, EM>::NZ;
       constexpr int NL = LocalBlock<EN, EM>::NL;
       int i, m, n, mu0, la0;
       pair_index(p, i, m, n, mu0, la0);
       const int em = D.eo[m], en = D.eb[n];
-      const double q1 = (bd[2 * p] + bs[2 * p] / B.Ds1) / B.E1;
-      const double q3 = (bd[2 * p + 1] + bs[2 * p + 1] / B.Ds3) / B.E3;
-      const double dpx = ox[NS * i], dpy = ox[NS * i + 1], dth = ox[NS * i + 3];
-      double v[NL];
-      for (int j = 0; j < EN; ++j) v[j] = (j < en ? bx[mu0 + j] : 0.0) + B.J1[j] * q1 + B.J3z[j] * q3;
-      for (int j = 0; j < EM; ++j) v[EN + j] = (j < em ? bx[la0 + j] : 0.0) + B.J1[EN + j] * q1 + B.J3z[EN + j] * q3;
       const int re = D.ePair + 2 * p;
-      v[NZ] = bc[re];
-      v[NZ + 1] = bc[re + 1];
+      // rhs loads issue with the block's own loads (before its factorization)
+      const double bd1 = bd[2 * p], bs1 = bs[2 * p], bd3 = bd[2 * p + 1], bs3 = bs[2 * p + 1];
+      const double bc0 = bc[re], bc1 = bc[re + 1];
+      const double dpx = ox[NS * i], dpy = ox[NS * i + 1], dth = ox[NS * i + 3];
+      double bxz[NZ];
+      for (int j = 0; j < EN; ++j) bxz[j] = bx[mu0 + (j < en ? j : 0)];
+      for (int j = 0; j < EM; ++j) bxz[EN + j] = bx[la0 + (j < em ? j : 0)];
+      LocalBlock<EN, EM> B;
+      build_local<EN, EM>(B, p, ls, dw, dc);
+      B.factor();
+      const double q1 = (bd1 + bs1 / B.Ds1) / B.E1;
+      const double q3 = (bd3 + bs3 / B.Ds3) / B.E3;
+      double v[NL];
+      for (int j = 0; j < EN; ++j) v[j] = (j < en ? bxz[j] : 0.0) + B.J1[j] * q1 + B.J3z[j] * q3;
+      for (int j = 0; j < EM; ++j) v[EN + j] = (j < em ? bxz[EN + j] : 0.0) + B.J1[EN + j] * q1 + B.J3z[EN + j] * q3;
+      v[NZ] = bc0;
+      v[NZ + 1] = bc1;
       for (int r = 0; r < NL; ++r) v[r] -= B.B[r][0] * dpx + B.B[r][1] * dpy + B.B[r][2] * dth;
       if (B.piv) {
         double vp[NL];
@@ -1207,12 +1268,12 @@ struct ObcaSolver {
         j1 += B.J1[r] * v[r];
         j3 += B.J3z[r] * v[r];
       }
-      const double y1 = (j1 - bd[2 * p] - bs[2 * p] / B.Ds1) / B.E1;
-      const double y3 = (j3 - bd[2 * p + 1] - bs[2 * p + 1] / B.Ds3) / B.E3;
+      const double y1 = (j1 - bd1 - bs1 / B.Ds1) / B.E1;
+      const double y3 = (j3 - bd3 - bs3 / B.Ds3) / B.E3;
       od[2 * p] = y1;
       od[2 * p + 1] = y3;
-      os[2 * p] = (bs[2 * p] + y1) / B.Ds1;
-      os[2 * p + 1] = (bs[2 * p + 1] + y3) / B.Ds3;
+      os[2 * p] = (bs1 + y1) / B.Ds1;
+      os[2 * p + 1] = (bs3 + y3) / B.Ds3;
     }
   }
 
@@ -2449,8 +2510,8 @@ struct ObcaSolver {
   HTP_HD HTP_FI void grad_lag_into(gd* out) {
     eval_jt(A(L.x), A(L.yc), A(L.yd), out);
     const gd* gf = A(L.gf);
-    HTP_UNROLL
-    for (int q = c.lane; q < D.n; q += c.width) out[q] += gf[q];
+    double a_[SW_U], b_[SW_U];
+    sweep(D.n, [&](int q, int k) { a_[k] = out[q]; b_[k] = gf[q]; }, [&](int q, int k) { out[q] = a_[k] + b_[k]; });
     c.sync();
   }
 
@@ -2863,12 +2924,20 @@ struct ObcaSolver {
       {
         const gd* gf = A(L.gf);
         const gd* yd = A(L.yd);
-        HTP_UNROLL
-        for (int q = c.lane; q < D.n; q += c.width) rx[q] = -(gl[q] - gf[q] + gbx[q]);
-        HTP_UNROLL
-        for (int r = c.lane; r < D.md; r += c.width) { rs[r] = -(gbs[r] - yd[r]); rd[r] = -(dd[r] - s[r]); }
-        HTP_UNROLL
-        for (int r = c.lane; r < D.mc; r += c.width) rc[r] = -cc[r];
+        {
+          double a_[SW_U], b_[SW_U], g_[SW_U];
+          sweep(D.n, [&](int q, int k) { a_[k] = gl[q]; b_[k] = gf[q]; g_[k] = gbx[q]; },
+                [&](int q, int k) { rx[q] = -(a_[k] - b_[k] + g_[k]); });
+        }
+        {
+          double a_[SW_U], b_[SW_U], d_[SW_U], s_[SW_U];
+          sweep(D.md, [&](int r, int k) { a_[k] = gbs[r]; b_[k] = yd[r]; d_[k] = dd[r]; s_[k] = s[r]; },
+                [&](int r, int k) { rs[r] = -(a_[k] - b_[k]); rd[r] = -(d_[k] - s_[k]); });
+        }
+        {
+          double a_[SW_U];
+          sweep(D.mc, [&](int r, int k) { a_[k] = cc[r]; }, [&](int r, int k) { rc[r] = -a_[k]; });
+        }
         c.sync();
       }
       double dw, dc;
@@ -2883,10 +2952,11 @@ struct ObcaSolver {
       const double phi = (mu_cache == mu) ? phi_cache : barrier(x, s, mu);
       const double theta = (theta_cache >= 0.0) ? theta_cache : theta_of(cc, dd, s);
       double gBD = 0.0;
-      HTP_UNROLL
-      for (int q = c.lane; q < D.n; q += c.width) gBD += gbx[q] * dx[q];
-      HTP_UNROLL
-      for (int r = c.lane; r < D.md; r += c.width) gBD += gbs[r] * ds[r];
+      {
+        double a_[SW_U], b_[SW_U];
+        sweep(D.n, [&](int q, int k) { a_[k] = gbx[q]; b_[k] = dx[q]; }, [&](int, int k) { gBD += a_[k] * b_[k]; });
+        sweep(D.md, [&](int r, int k) { a_[k] = gbs[r]; b_[k] = ds[r]; }, [&](int, int k) { gBD += a_[k] * b_[k]; });
+      }
       gBD = c.sum(gBD);
       const double alpha_max = frac_primal(dx, ds);
       double a_min = o.gamma_theta;
@@ -2898,17 +2968,20 @@ struct ObcaSolver {
       auto is_ftype = [&](double a) { return gBD < 0 && a * pow(-gBD, o.s_phi) > o.delta * pow(theta, o.s_theta); };
       // keep the Newton rhs (x part) for SOC solves: copy into sx after gbx is consumed
       gd* rxk = A(L.sx);
-      HTP_UNROLL
-      for (int q = c.lane; q < D.n; q += c.width) rxk[q] = rx[q];
+      {
+        double a_[SW_U];
+        sweep(D.n, [&](int q, int k) { a_[k] = rx[q]; }, [&](int q, int k) { rxk[q] = a_[k]; });
+      }
       c.sync();
       gd* xt = A(L.xt); gd* st = A(L.st);
       double alpha = alpha_max, a_primal = alpha, a_test = alpha, th_t = 0, ph_t = 0, th_acc = 0;
       bool accepted = false, soc_used = false, first = true;
       while (alpha >= a_min) {
-        HTP_UNROLL
-        for (int q = c.lane; q < D.n; q += c.width) xt[q] = x[q] + alpha * dx[q];
-        HTP_UNROLL
-        for (int r = c.lane; r < D.md; r += c.width) st[r] = s[r] + alpha * ds[r];
+        {
+          double a_[SW_U], b_[SW_U];
+          sweep(D.n, [&](int q, int k) { a_[k] = x[q]; b_[k] = dx[q]; }, [&](int q, int k) { xt[q] = a_[k] + alpha * b_[k]; });
+          sweep(D.md, [&](int r, int k) { a_[k] = s[r]; b_[k] = ds[r]; }, [&](int r, int k) { st[r] = a_[k] + alpha * b_[k]; });
+        }
         c.sync();
         if (acceptable(alpha, xt, st, phi, theta, gBD, is_ftype(alpha), th_t, ph_t)) {
           accepted = true; a_primal = alpha; a_test = alpha; th_acc = th_t;
@@ -3022,10 +3095,9 @@ struct ObcaSolver {
       }
       {  // constraint values at the new point = those of the accepted trial point
         const gd* ct = A(L.ct); const gd* dtv = A(L.dt);
-        HTP_UNROLL
-        for (int r = c.lane; r < D.mc; r += c.width) cc[r] = ct[r];
-        HTP_UNROLL
-        for (int r = c.lane; r < D.md; r += c.width) dd[r] = dtv[r];
+        double a_[SW_U];
+        sweep(D.mc, [&](int r, int k) { a_[k] = ct[r]; }, [&](int r, int k) { cc[r] = a_[k]; });
+        sweep(D.md, [&](int r, int k) { a_[k] = dtv[r]; }, [&](int r, int k) { dd[r] = a_[k]; });
       }
       phi_cache = ph_t;
       mu_cache = mu;
