@@ -694,14 +694,28 @@ struct ObcaSolver {
       const gd* Gn = gp(in.bodyG) + 2 * D.offb[n];
       const gd* gn = gp(in.bodyg) + D.offb[n];
       const int re = D.ePair + 2 * p;
+      // loads first (indices clamped), stores after
+      double g0[EN_], g1[EN_], gj[EN_];
+      for (int j = 0; j < EN_; ++j) {
+        const int jj = j < en ? j : 0;
+        g0[j] = Gn[2 * jj]; g1[j] = Gn[2 * jj + 1]; gj[j] = gn[jj];
+      }
+      double a0v[EM_], a1v[EM_], bj[EM_];
+      for (int j = 0; j < EM_; ++j) {
+        const int jj = j < em ? j : 0;
+        a0v[j] = Am[2 * jj]; a1v[j] = Am[2 * jj + 1]; bj[j] = bm[jj];
+      }
       const double ya = scE[re] * yc[re], yb = scE[re + 1] * yc[re + 1];
       const double y1 = scI[2 * p] * yd[2 * p], y3 = scI[2 * p + 1] * yd[2 * p + 1];
-      for (int j = 0; j < en; ++j) out[mu0 + j] = Gn[2 * j] * ya + Gn[2 * j + 1] * yb - gn[j] * y3;
       const double tx = x[NS * i], ty = x[NS * i + 1];
-      for (int j = 0; j < em; ++j) {
-        const double a0 = Am[2 * j], a1 = Am[2 * j + 1];
-        out[la0 + j] = (cs * a0 + sn * a1) * ya + (-sn * a0 + cs * a1) * yb + 2.0 * (a0 * w[0] + a1 * w[1]) * y1 +
-                       (a0 * tx + a1 * ty - bm[j]) * y3;
+      for (int j = 0; j < EN_; ++j)
+        if (j < en) out[mu0 + j] = g0[j] * ya + g1[j] * yb - gj[j] * y3;
+      for (int j = 0; j < EM_; ++j) {
+        if (j < em) {
+          const double a0 = a0v[j], a1 = a1v[j];
+          out[la0 + j] = (cs * a0 + sn * a1) * ya + (-sn * a0 + cs * a1) * yb + 2.0 * (a0 * w[0] + a1 * w[1]) * y1 +
+                         (a0 * tx + a1 * ty - bj[j]) * y3;
+        }
       }
       pr[3 * p + 0] = w[0] * y3;
       pr[3 * p + 1] = w[1] * y3;
@@ -715,30 +729,35 @@ struct ObcaSolver {
         for (int k = 0; k < NS; ++k) gx[k] += scE[k] * yc[k];
       else
         for (int k = 0; k < NS; ++k) gx[k] += scE[D.eDyn + NS * (i - 1) + k] * yc[D.eDyn + NS * (i - 1) + k];
+      // every store of the stage goes after its last load (the pairR gathers)
+      double tt[NS], gw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       if (i == N - 1) {
         for (int k = 0; k < NS; ++k) {
-          const double t = scE[D.eTerm + k] * yc[D.eTerm + k];
-          gx[k] += t;
-          if constexpr (!PT) out[D.oS + k] = t;
+          tt[k] = scE[D.eTerm + k] * yc[D.eTerm + k];
+          gx[k] += tt[k];
         }
       } else {
         double w[8], J[40], yy[5];
         stage_w(x, i, w);
         dynJ(w, J);
         for (int k = 0; k < NS; ++k) yy[k] = scE[D.eDyn + NS * i + k] * yc[D.eDyn + NS * i + k];
-        double gw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int k = 0; k < NS; ++k)
           for (int j = 0; j < D.nw; ++j) gw[j] -= J[k * D.nw + j] * yy[k];
         for (int k = 0; k < NS; ++k) gx[k] += gw[k];
-        out[D.oU + NC * i] = gw[5];
-        out[D.oU + NC * i + 1] = gw[6];
-        if (D.topt) out[D.oTAU + i] = gw[7];
       }
       for (int q = 0; q < MK; ++q) {
         const int p = blk(i, q);
         gx[0] += pr[3 * p];
         gx[1] += pr[3 * p + 1];
         gx[3] += pr[3 * p + 2];
+      }
+      if (i == N - 1) {
+        if constexpr (!PT)
+          for (int k = 0; k < NS; ++k) out[D.oS + k] = tt[k];
+      } else {
+        out[D.oU + NC * i] = gw[5];
+        out[D.oU + NC * i + 1] = gw[6];
+        if (D.topt) out[D.oTAU + i] = gw[7];
       }
       for (int k = 0; k < NS; ++k) out[NS * i + k] = gx[k];
     }
@@ -1536,35 +1555,50 @@ struct ObcaSolver {
     const gd* PS = A(L.pairS);
     gd* K = A(L.Kst) + (int64_t)i * nb * nb;
     const double dT = par(P_DT);
-    for (int q = 0; q < nb * nb; ++q) K[q] = 0.0;
+    // The block is accumulated in registers (lower triangle, compile-time indices: every
+    // add() site is unrolled) and stored once at the end: a read-modify-write of K in HBM
+    // per contribution cost one memory round trip each.  (r, q) and (q, r) receive the
+    // same adds in the same order, so the mirrored store is the plain accumulation.
+    constexpr int NT = NBMAX * (NBMAX + 1) / 2;
+    double Kl[NT];
+    for (int e = 0; e < NT; ++e) Kl[e] = 0.0;
     auto add = [&](int r, int q, double v) {
-      K[r * nb + q] += v;
-      if (r != q) K[q * nb + r] += v;
+      const int hi = r >= q ? r : q, lo = r >= q ? q : r;
+      Kl[hi * (hi + 1) / 2 + lo] += v;
     };
-    for (int k = 0; k < NS; ++k) add(k, k, -dc);
     const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
-    for (int k = 0; k < NS; ++k) add(k, NS + k, scE[rowbase + k]);
-    // variables of this block
+    // variables of this block; their bound data load up front (indices clamped)
     int vidx[8];
     int nv = (i < N - 1) ? D.nw : NS;
     for (int k = 0; k < NS; ++k) vidx[k] = NS * i + k;
+    vidx[5] = vidx[6] = vidx[7] = NS * i;
     if (i < N - 1) {
       vidx[5] = D.oU + NC * i;
       vidx[6] = D.oU + NC * i + 1;
       if (D.topt) vidx[7] = D.oTAU + i;
     }
-    for (int a = 0; a < nv; ++a) {
+    double xq[8], xlq[8], xuq[8], zlq[8], zuq[8], sce[NS];
+    for (int a = 0; a < 8; ++a) {
       const int q = vidx[a];
-      double dg;
-      if (ls) dg = 1.0;
-      else {
-        dg = dw;
-        if (finite_(xL[q])) dg += zL[q] / (x[q] - xL[q]);
-        if (finite_(xU[q])) dg += zU[q] / (xU[q] - x[q]);
-      }
-      add(NS + a, NS + a, dg);
+      xq[a] = x[q]; xlq[a] = xL[q]; xuq[a] = xU[q]; zlq[a] = zL[q]; zuq[a] = zU[q];
     }
-    for (int a = nv; a < D.nw; ++a) add(NS + a, NS + a, 1.0);  // padding (last stage)
+    for (int k = 0; k < NS; ++k) sce[k] = scE[rowbase + k];
+    for (int k = 0; k < NS; ++k) add(k, k, -dc);
+    for (int k = 0; k < NS; ++k) add(k, NS + k, sce[k]);
+    for (int a = 0; a < 8; ++a) {
+      if (a < nv) {
+        double dg;
+        if (ls) dg = 1.0;
+        else {
+          dg = dw;
+          if (finite_(xlq[a])) dg += zlq[a] / (xq[a] - xlq[a]);
+          if (finite_(xuq[a])) dg += zuq[a] / (xuq[a] - xq[a]);
+        }
+        add(NS + a, NS + a, dg);
+      }
+    }
+    for (int a = 0; a < 8; ++a)
+      if (a >= nv && a < D.nw) add(NS + a, NS + a, 1.0);  // padding (last stage)
     if (PT && !ls && i < N - 1) {  // optimizer_points.py objective: 20 (v dT)^2, (u_{i+1} - u_i)^2
       const int U0 = NS + 5, V0 = NS + 2;
       add(V0, V0, sf * 40.0 * dT * dT);
@@ -1619,8 +1653,9 @@ struct ObcaSolver {
       stage_w(x, i, w);
       for (int k = 0; k < NS; ++k) yy[k] = -scE[D.eDyn + NS * i + k] * yc[D.eDyn + NS * i + k];
       dynH(w, yy, H);
-      for (int r = 0; r < D.nw; ++r)
-        for (int q = 0; q <= r; ++q) add(NS + r, NS + q, H[r * (r + 1) / 2 + q]);
+      for (int r = 0; r < 8; ++r)
+        if (r < D.nw)
+          for (int q = 0; q <= r; ++q) add(NS + r, NS + q, H[r * (r + 1) / 2 + q]);
     } else if (!ls && i >= 1 && i - 1 < N - 2) {
       // last stage has no u; nothing else
     }
@@ -1644,6 +1679,9 @@ struct ObcaSolver {
         add(NS + k, NS + k, st * st / Et);
       }
     }
+    for (int r = 0; r < NBMAX; ++r)
+      for (int q = 0; q < NBMAX; ++q)
+        if (r < nb && q < nb) K[r * nb + q] = Kl[r >= q ? r * (r + 1) / 2 + q : q * (q + 1) / 2 + r];
     // Riccati records: reciprocal scaling of this stage's multiplier rows
     {
       gd* Ss = A(L.LD) + (int64_t)i * nb * nb + SOFF;
