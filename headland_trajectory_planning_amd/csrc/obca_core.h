@@ -2426,29 +2426,33 @@ struct ObcaSolver {
     const int MK = blocks_per_stage();
     const double Hs = ls ? 1.0 : 10000.0 * sf + dw;
     for (int i = c.lane; i < N; i += c.width) {
+      // the stage rhs is built in registers and stored once (no read-modify-write in HBM)
       gd* r = V + (int64_t)i * nb;
       const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
-      for (int k = 0; k < NS; ++k) r[k] = bc[rowbase + k];
-      for (int k = 0; k < NS; ++k) r[NS + k] = bx[NS * i + k];
+      double rv[NBMAX];
+      for (int k = 0; k < NS; ++k) rv[k] = bc[rowbase + k];
+      for (int k = 0; k < NS; ++k) rv[NS + k] = bx[NS * i + k];
+      for (int a = NS; a < NBMAX - NS; ++a) rv[NS + a] = 0.0;
       if (i < N - 1) {
-        r[NS + 5] = bx[D.oU + NC * i];
-        r[NS + 6] = bx[D.oU + NC * i + 1];
-        if (D.topt) r[NS + 7] = bx[D.oTAU + i];
+        rv[NS + 5] = bx[D.oU + NC * i];
+        rv[NS + 6] = bx[D.oU + NC * i + 1];
+        if (D.topt) rv[NS + 7] = bx[D.oTAU + i];
       } else {
-        for (int a = NS; a < D.nw; ++a) r[NS + a] = 0.0;
         if constexpr (!PT)
           for (int k = 0; k < NS; ++k) {
             const double st = scE[D.eTerm + k];
             const double Et = dc + st * st / Hs;
-            r[NS + k] -= st / Et * (st * bx[D.oS + k] / Hs - bc[D.eTerm + k]);
+            rv[NS + k] -= st / Et * (st * bx[D.oS + k] / Hs - bc[D.eTerm + k]);
           }
       }
       for (int q = 0; q < MK; ++q) {
         const int p = blk(i, q);
-        r[NS + 0] += PR[3 * p];
-        r[NS + 1] += PR[3 * p + 1];
-        r[NS + 3] += PR[3 * p + 2];
+        rv[NS + 0] += PR[3 * p];
+        rv[NS + 1] += PR[3 * p + 1];
+        rv[NS + 3] += PR[3 * p + 2];
       }
+      for (int a = 0; a < NBMAX; ++a)
+        if (a < nb) r[a] = rv[a];
     }
     if constexpr (PT)
       for (int e = c.lane; e < nb; e += c.width) V[(int64_t)N * nb + e] = (e < NS) ? bc[D.eTerm + e] : 0.0;
