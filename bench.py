@@ -149,7 +149,7 @@ def main():
     # HBM bytes per launch measured with rocprofv3 PMC passes (tools/profile.sh ->
     # profiles/*_traffic.json) for this exact workload; scaled to this launch's
     # iteration count (bytes per problem-iteration x iterations).
-    tf = os.environ.get("HTP_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r01c_traffic.json"))
+    tf = os.environ.get("HTP_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r01d_traffic.json"))
     if tf and os.path.exists(tf):
         tj = json.load(open(tf))
         if tj.get("workload") == args.config and tj.get("batch") == B and tj.get("bytes_per_problem_iter"):
