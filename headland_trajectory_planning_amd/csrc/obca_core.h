@@ -2198,6 +2198,14 @@ struct ObcaSolver {
     if (N >= 2)
       for (int u = 0; u < PB; ++u)
         if (c.lane + u * c.width < RB) buf0[c.lane + u * c.width] = rec_get(db[u], N - 2, V, X);
+    // records are gathered two stages ahead of use: the one of stage i-1 (preA) was issued
+    // during stage i+1, so a full stage of latency is hidden behind this one's work
+    // (backward records read only LD and V, which the pass does not write)
+    double preA[PB];
+    for (int u = 0; u < PB; ++u) {
+      const int e = c.lane + u * c.width;
+      preA[u] = (N >= 3 && e < RB) ? rec_get(db[u], N - 3, V, X) : 0.0;
+    }
     c.sync();
     HTP_PROF0();
     for (int i = N - 2; i >= 0; --i) {
@@ -2206,7 +2214,7 @@ struct ObcaSolver {
       double pre[PB];
       for (int u = 0; u < PB; ++u) {
         const int e = c.lane + u * c.width;
-        pre[u] = (i > 0 && e < RB) ? rec_get(db[u], i - 1, V, X) : 0.0;
+        pre[u] = (i > 1 && e < RB) ? rec_get(db[u], i - 2, V, X) : 0.0;
       }
       for (int r = c.lane; r < nz; r += c.width) {  // w = p - P e
         double acc = pv[r];
@@ -2243,8 +2251,9 @@ struct ObcaSolver {
       if (i > 0)
         for (int u = 0; u < PB; ++u) {
           const int e = c.lane + u * c.width;
-          if (e < RB) nxt[e] = pre[u];
+          if (e < RB) nxt[e] = preA[u];
         }
+      for (int u = 0; u < PB; ++u) preA[u] = pre[u];
       c.sync();
     }
     HTP_PROF(6);
@@ -2255,6 +2264,13 @@ struct ObcaSolver {
     }
     for (int u = 0; u < PB; ++u)
       if (c.lane + u * c.width < RF) buf0[c.lane + u * c.width] = rec_get(dfw[u], 0, V, X);
+    // two stages ahead, as in the backward pass: the record of stage i+2 reads X_{i+2}
+    // (p, rt of the backward pass), which this pass overwrites only at stage i+2
+    double preF[PB];
+    for (int u = 0; u < PB; ++u) {
+      const int e = c.lane + u * c.width;
+      preF[u] = (1 < N && e < RF) ? rec_get(dfw[u], 1, V, X) : 0.0;
+    }
     c.sync();
     for (int i = 0; i < N; ++i) {
       ld* cur = (i & 1) ? buf1 : buf0;
@@ -2262,7 +2278,7 @@ struct ObcaSolver {
       double pre[PB];
       for (int u = 0; u < PB; ++u) {
         const int e = c.lane + u * c.width;
-        pre[u] = (i + 1 < N && e < RF) ? rec_get(dfw[u], i + 1, V, X) : 0.0;
+        pre[u] = (i + 2 < N && e < RF) ? rec_get(dfw[u], i + 2, V, X) : 0.0;
       }
       for (int k = c.lane; k < NS; k += c.width) {
         double acc = cur[40 + k];
@@ -2309,9 +2325,10 @@ struct ObcaSolver {
         for (int k = c.lane; k < nz; k += c.width, ++un) zv[k] = zn[un];
         for (int u = 0; u < PB; ++u) {
           const int e = c.lane + u * c.width;
-          if (e < RF) nxt[e] = pre[u];
+          if (e < RF) nxt[e] = preF[u];
         }
       }
+      for (int u = 0; u < PB; ++u) preF[u] = pre[u];
       c.sync();
     }
     HTP_PROF(7);
