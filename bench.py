@@ -2,11 +2,12 @@
 
 Workload (BASELINE.json configs[3], "D"): randomized row-spacing / heading
 headlands, horizon N=80, M=6 convex obstacles, K=1 vehicle body, time-scaling
-on; 4096 problems per GPU (weak scaling: 32768 at 8 GPUs).  A "step" is one
-batched solve of all of a rank's problems to IPOPT convergence
-(libhtp.so htp_obca_solve_batch_device, inputs resident in HBM).
+on; the config's global batch of 32768 problems split over the GPUs (strong
+scaling: all 32768 on one GPU, 4096 per GPU at 8).  A "step" is one batched
+solve of all of a rank's problems to IPOPT convergence (libhtp.so
+htp_obca_solve_batch_device, inputs resident in HBM).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config D]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch GLOBAL_B] [--config D]
 
 Multi-GPU: launched by torch.distributed.run, one process per GPU; each rank
 solves its own contiguous slice of problem ids (no data-path collective); the
@@ -44,25 +45,51 @@ def make_batch(pids, N, M, imp, procs=16):
         return pool.map(_gen, [(p, N, M, imp) for p in pids], chunksize=32)
 
 
-def cpu_baseline(N, M, imp, budget_s=25.0):
-    """Oracle ("port"): numpy IPOPT restatement with the structured KKT solve,
-    one core, on the first problems of the same workload until the budget."""
-    from oracle.ipm import IpoptRestatement
-    from oracle.nlp import ObcaNLP
-    from oracle.structured import StructuredKKT
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(pk, budget_s=20.0):
+    """SURVEY 8(d) CPU baseline: the build's own C++ implementation of the same
+    solver (csrc/htp_cpu.cpp = obca_core.h compiled with g++ -O3 -fopenmp, one
+    problem per OpenMP thread, dynamic schedule) on this box's host cores, over
+    the first problems of the same packed workload, in chunks until the budget."""
+    import ctypes
+    so = os.path.join(ROOT, "headland_trajectory_planning_amd", "libhtp_cpu.so")
+    lib = ctypes.CDLL(so)
+    lib.htp_cpu_obca_solve_range.argtypes = [ctypes.POINTER(_native.ObcaBatch), ctypes.POINTER(_native.ObcaResult),
+                                             ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
+    lib.htp_cpu_obca_solve_range.restype = ctypes.c_int
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        threads = os.cpu_count() or 1
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    res = _native.HostResults(pk.batch, pk.n_var)
+    b, r = pk.struct(), res.struct()
     t0 = time.perf_counter()
-    done = 0
-    iters = 0
-    while time.perf_counter() - t0 < budget_s and done < 8:
-        inst = synth.make_instance(done, N=N, M=M, implement=imp)
-        nlp = ObcaNLP(inst)
-        sol = IpoptRestatement(nlp, kkt=StructuredKKT(nlp)).solve()
-        iters += sol["iters"]
-        done += 1
+    done, chunk = 0, threads
+    while done < pk.batch and time.perf_counter() - t0 < budget_s:
+        n = min(chunk, pk.batch - done)
+        if lib.htp_cpu_obca_solve_range(ctypes.byref(b), ctypes.byref(r), done, n, threads) != 0:
+            raise RuntimeError("htp_cpu_obca_solve_range failed")
+        done += n
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "solves/s", "cores": 1, "kind": "port",
-            "sample": f"{done} problem(s) (pids 0..{done - 1}) of the same workload solved to convergence by "
-                      f"oracle/ipm.py + oracle/structured.py (numpy, 1 core) in {dt:.1f} s; {iters} IPM iterations"}
+    st = res.status[:done]
+    return {"value": done / dt, "unit": "solves/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+            "success_rate": float(np.isin(st, [0, 1]).mean()) if done else None,
+            "sample": f"first {done} problems (pids 0..{done - 1}) of the same workload solved to convergence by "
+                      f"libhtp_cpu.so (obca_core.h, g++ -O3 -fopenmp, {threads} threads, one problem per thread) "
+                      f"in {dt:.1f} s; {int(res.iterations[:done].sum())} IPM iterations. History: the reference's "
+                      f"CasADi/IPOPT solve of its N=66 notebook problem took 0.213 s setup + 2.662 s solve "
+                      f"(R/test/obca.ipynb:400,405; 0.35 solves/s/core, unknown CPU)"}
 
 
 def main():
@@ -71,9 +98,10 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="D")
-    ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="global batch split over the ranks (default: the config's BASELINE batch, D = 32768)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=25.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--gen-procs", type=int, default=16, help="CPU worker processes for instance generation")
     args = ap.parse_args()
 
@@ -88,9 +116,10 @@ def main():
         dist.init_process_group(backend="nccl", init_method="env://")
     dev = torch.device("cuda", local)
 
-    _, N, M, imp = synth.CONFIGS[args.config]
-    B = args.batch
-    pids = sharding.rank_pids(rank, B)
+    Bcfg, N, M, imp = synth.CONFIGS[args.config]
+    GB = args.batch or Bcfg
+    pids = sharding.rank_slice(rank, world, GB)
+    B = len(pids)
     t = time.perf_counter()
     insts = make_batch(pids, N, M, imp, args.gen_procs)
     gen_s = time.perf_counter() - t
@@ -136,7 +165,7 @@ def main():
     st_np = status.cpu().numpy()
     elapsed, all_iters, all_ok = sharding.reduce_stats(dist, dev, elapsed, float(it_np.sum()),
                                                        float(np.isin(st_np, [0, 1]).sum()))
-    total_solves = B * world * args.steps
+    total_solves = GB * args.steps
     value = total_solves / elapsed
 
     topt = pk.time_opt
@@ -149,30 +178,33 @@ def main():
     # HBM bytes per launch measured with rocprofv3 PMC passes (tools/profile.sh ->
     # profiles/*_traffic.json) for this exact workload; scaled to this launch's
     # iteration count (bytes per problem-iteration x iterations).
-    tf = os.environ.get("HTP_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r01d_traffic.json"))
+    tf = os.environ.get("HTP_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r02_traffic.json"))
     if tf and os.path.exists(tf):
         tj = json.load(open(tf))
-        if tj.get("workload") == args.config and tj.get("batch") == B and tj.get("bytes_per_problem_iter"):
+        if tj.get("workload") == args.config and tj.get("batch") == B and tj.get("bytes_per_problem_iter") \
+                and tj.get("solver_sha") == _native.core_sha():
             traffic = tj["bytes_per_problem_iter"] * float(it_np.sum())
 
     line = {
         "metric": "headland-turn solves/sec (batch, N=80, 6 obs) at 1/2/4/8 MI355X",
         "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (Philox-seeded orchard headlands, synth.py)",
-        "config": {"workload": f"config {args.config}: {B} problems/GPU, N={N} horizon, M={M} obstacles, "
-                               f"K={pk.K} bodies ({imp}), time-opt on; IPOPT-restated IPM to tol 1e-8",
-                   "batch_per_gpu": B, "global_batch": B * world, "N": N, "M": M, "K": pk.K,
+        "config": {"workload": f"config {args.config}: global batch {GB} split over {world} GPU(s) ({B} on rank 0), "
+                               f"N={N} horizon, M={M} obstacles, K={pk.K} bodies ({imp}), time-opt on; "
+                               f"IPOPT-restated IPM to tol 1e-8",
+                   "batch_per_gpu": B, "global_batch": GB, "N": N, "M": M, "K": pk.K,
                    "parallelism": f"problem-sharded x{world}"},
-        "solver": {"success_rate": all_ok / (B * world), "mean_iters": all_iters / (B * world),
+        "solver": {"success_rate": all_ok / GB, "mean_iters": all_iters / GB,
                    "p99_iters_rank0": float(np.percentile(it_np, 99)), "max_iters_rank0": int(it_np.max()),
                    "gen_s": gen_s},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "hbm", "limiter": "latency: one wavefront per problem, the slowest solve sets the launch",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_iter_per_problem": biter, "kernel_ms_avg": avg_ms},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(N, M, imp, args.cpu_budget)
+        line["cpu_baseline"] = cpu_baseline(pk, args.cpu_budget)
     if rank == 0:
         print(json.dumps(line, default=float), flush=True)
     if dist:

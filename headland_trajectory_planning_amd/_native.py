@@ -150,6 +150,16 @@ def _declare(lib):
 _LIB = None
 
 
+def core_sha():
+    """Short hash of the OBCA solver sources (ties profiles/*_traffic.json to a solver version)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("obca_core.h", "htp_common.h", "htp_obca.hip", "dyn_gen.h", "wave_ctx.h"):
+        with open(os.path.join(HERE, "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
 def load(path=LIB_PATH):
     """Load the in-tree HIP library; raise loudly if it is absent."""
     global _LIB

@@ -1,0 +1,55 @@
+// CPU baseline build of the OBCA interior-point core ("the
+// build's own C++ CPU implementation of the same solver, OpenMP, one problem
+// per core, on all host cores").  Same obca_core.h as the gfx950 kernel, run
+// as a serial lane per OpenMP thread.  Loaded only by bench.py's cpu_baseline
+// leg; the product path never calls it (there is no CPU fallback).
+#include <omp.h>
+
+#include <cstdlib>
+#include <vector>
+
+#define HTP_HD
+#include "wave_ctx.h"
+#include "obca_batch.h"
+
+using namespace htp;
+
+extern "C" int htp_cpu_threads(void) { return omp_get_max_threads(); }
+
+// Solves problems [first, first + count) of the batch; returns 0 or < 0 on bad input.
+extern "C" int htp_cpu_obca_solve_range(const htp_obca_batch* in, htp_obca_result* out, int64_t first,
+                                        int64_t count, int nthreads) {
+  const char* e = nullptr;
+  if (check_shape(in, &e) || first < 0 || first + count > in->batch) return -1;
+  const Options o = default_options();
+  Dims D;
+  make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
+  const Layout L = make_layout(D);
+  const BatchView b{in->traj, in->obs_A, in->obs_b, in->body_G, in->body_g, in->params,
+                    in->init_control, in->init_mu, in->init_lambda};
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads)
+  {
+    std::vector<double> ws((size_t)L.total);
+    std::vector<double> lds(4 * NBMAX * NBMAX + 8 + 128);
+    std::vector<int> ilds(2 * NBMAX);
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t p = first; p < first + count; ++p) {
+      HostLane c;
+      c.lds = lds.data();
+      c.ildsp = ilds.data();
+      const ProblemIn pin = problem_view(b, D, p);
+      ObcaSolver<HostLane, MAXE, MAXE> S(c, D, L, o, pin, ws.data());
+      Result r{};
+      S.run(r);
+      if (out->x)
+        for (int q = 0; q < D.n; ++q) out->x[(size_t)p * D.n + q] = ws[L.x + q];
+      if (out->objective) out->objective[p] = r.objective;
+      if (out->status) out->status[p] = r.status;
+      if (out->iterations) out->iterations[p] = r.iters;
+      if (out->n_factor) out->n_factor[p] = r.n_factor;
+      if (out->nlp_error) out->nlp_error[p] = r.nlp_error;
+    }
+  }
+  return 0;
+}

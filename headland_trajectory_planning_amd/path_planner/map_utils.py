@@ -10,6 +10,16 @@ LEAVE_POSE = 1
 ENTER_POSE = 2
 
 
+def plot_arrow(x, y, yaw, plt=None, length=1.0, width=0.5, fc="r", ec="k"):
+    """Heading arrow(s) on a matplotlib axes (map_utils.py:14-31); plotting only."""
+    if not isinstance(x, float):
+        for ix, iy, iyaw in zip(x, y, yaw):
+            plot_arrow(float(ix), float(iy), float(iyaw), plt, length, width, fc, ec)
+        return
+    plt.arrow(x, y, length * np.cos(yaw), length * np.sin(yaw), fc=fc, ec=ec, head_width=width, head_length=width)
+    plt.plot(x, y)
+
+
 def create_tree_rows(row_num, row_width, row_lengths, slope_angle=0, l_std=0.0):
     tree_rows = []
     delta_x = row_width * np.tan(slope_angle)

@@ -1,7 +1,7 @@
 """Problem sharding across GPUs (one process per GPU).
 
-Problems are independent, so rank r of W solves the contiguous id slice
-[r*B, (r+1)*B) (weak scaling: B problems per GPU).  Problem ids seed the
+Problems are independent, so rank r of W solves a contiguous slice of the
+global id range [0, B) (rank_slice: sizes differ by at most one).  Problem ids seed the
 generator (Philox key [20251015, pid]), so a problem is identical at any world
 size.  The only collectives are the timing barrier and these two tiny
 reductions (RCCL on GPUs, gloo on CPU); nothing is exchanged on the data path.
@@ -10,6 +10,13 @@ reductions (RCCL on GPUs, gloo on CPU); nothing is exchanged on the data path.
 
 def rank_pids(rank, per_rank):
     return list(range(rank * per_rank, (rank + 1) * per_rank))
+
+
+def rank_slice(rank, world, total):
+    """Contiguous slice of [0, total) for `rank` of `world` (balanced to +-1)."""
+    lo = rank * total // world
+    hi = (rank + 1) * total // world
+    return list(range(lo, hi))
 
 
 def reduce_stats(dist, device, elapsed, iters_sum, ok_sum):
