@@ -15,7 +15,8 @@ NPARAM = 24
  P_MAXV, P_MAXACC, P_MAXSR, P_DMIN, P_XLO, P_XHI, P_YLO, P_YHI, P_HAS_INIT_CONTROL, P_HAS_INIT_DUAL) = range(23)
 
 STATUS_STR = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Maximum_Iterations_Exceeded",
-              3: "Restoration_Failed", 4: "Error_In_Step_Computation", 5: "Invalid_Problem_Definition"}
+              3: "Restoration_Failed", 4: "Error_In_Step_Computation", 5: "Invalid_Problem_Definition",
+              6: "Maximum_CpuTime_Exceeded", 7: "Infeasible_Problem_Detected", 8: "Search_Direction_Becomes_Too_Small"}
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int32)
@@ -31,7 +32,8 @@ class ObcaBatch(ctypes.Structure):
 
 class ObcaResult(ctypes.Structure):
     _fields_ = [("x", ctypes.c_void_p), ("objective", ctypes.c_void_p), ("status", ctypes.c_void_p),
-                ("iterations", ctypes.c_void_p), ("n_factor", ctypes.c_void_p), ("nlp_error", ctypes.c_void_p)]
+                ("iterations", ctypes.c_void_p), ("n_factor", ctypes.c_void_p), ("nlp_error", ctypes.c_void_p),
+                ("n_resto", ctypes.c_void_p)]
 
 
 class RsPaths(ctypes.Structure):
@@ -397,10 +399,11 @@ class HostResults:
         self.iterations = np.zeros(batch, dtype=np.int32)
         self.n_factor = np.zeros(batch, dtype=np.int32)
         self.nlp_error = np.zeros(batch)
+        self.n_resto = np.zeros(batch, dtype=np.int32)
 
     def struct(self):
         r = ObcaResult()
-        for name in ("x", "objective", "status", "iterations", "n_factor", "nlp_error"):
+        for name in ("x", "objective", "status", "iterations", "n_factor", "nlp_error", "n_resto"):
             setattr(r, name, getattr(self, name).ctypes.data)
         return r
 

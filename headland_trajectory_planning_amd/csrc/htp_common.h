@@ -37,6 +37,14 @@ struct Options {
   double mu_init, kappa_eps, kappa_mu, theta_mu, tau_min, kappa_sigma, kappa_d, s_max;
   double gamma_theta, gamma_phi, delta, s_theta, s_phi, eta_phi, alpha_min_frac, kappa_soc;
   double dw0, dw_min, dw_max, kw_minus, kw_plus, kw_plus_bar, dc_bar, kappa_c;
+  // line-search heuristics and the restoration phase (oracle/ipm.py docstring)
+  double obj_max_inc, tiny_step_tol, tiny_step_y_tol, soft_resto_pderror_reduction_factor;
+  double resto_penalty_parameter, resto_proximity_weight, required_infeasibility_reduction;
+  double bound_mult_reset_threshold;
+  int max_filter_resets, filter_reset_trigger, watchdog_shortened_iter_trigger, watchdog_trial_iter_max;
+  int max_soft_resto_iters, pad1;
+  // max_cpu_time (optimizer.py:475,486): seconds per problem, <= 0 = off; wall_rate = device wall-clock ticks/s
+  double max_cpu_time, wall_rate;
 };
 
 inline Options default_options() {
@@ -52,6 +60,13 @@ inline Options default_options() {
   o.eta_phi = 1e-8; o.alpha_min_frac = 0.05; o.kappa_soc = 0.99;
   o.dw0 = 1e-4; o.dw_min = 1e-20; o.dw_max = 1e40; o.kw_minus = 1.0 / 3.0; o.kw_plus = 8.0;
   o.kw_plus_bar = 100.0; o.dc_bar = 1e-8; o.kappa_c = 0.25;
+  o.obj_max_inc = 5.0; o.tiny_step_tol = 10.0 * 2.220446049250313e-16; o.tiny_step_y_tol = 1e-2;
+  o.soft_resto_pderror_reduction_factor = 0.9999; o.max_soft_resto_iters = 10;
+  o.resto_penalty_parameter = 1000.0; o.resto_proximity_weight = 1.0; o.required_infeasibility_reduction = 0.9;
+  o.bound_mult_reset_threshold = 1000.0;
+  o.max_filter_resets = 5; o.filter_reset_trigger = 5; o.watchdog_shortened_iter_trigger = 10;
+  o.watchdog_trial_iter_max = 3;
+  o.max_cpu_time = 0.0; o.wall_rate = 1.0;
   return o;
 }
 
@@ -77,6 +92,15 @@ struct Layout {
   int64_t pairS, pairR;                                      // 6P, 3P
   int64_t Kst, Off, LD, fac, V, X;                           // stage storage
   int64_t ipiv;                                              // ints stored as double
+  // restoration phase: n/p variables R = [n_c | p_c | n_d | p_d] (nR = 2 mc + 2 md), their trial values,
+  // steps, bound multipliers and multiplier steps; per-row diagonal eR (mc + md) of the eliminated n/p;
+  // folded constraint right-hand sides; the reference point x_R and D_R = 1/max(1,|x_R|) (n)
+  int64_t R, Rt, dR, zR, dzR, eR, rcf, rdf, xR, dr, rRx;
+  // the original iterate while the restoration phase runs; the original filter (2 FMAX); saved scalars
+  int64_t ox, os, oyc, oyd, ozL, ozU, ovL, ovU, ofilt, osv;
+  // watchdog reference point and direction (x, s, y, z, v, R, zR, c, d, step)
+  int64_t wx, ws, wyc, wyd, wzL, wzU, wvL, wvU, wR, wzR, wc, wd, wdx, wds, wdyc, wdyd, wdR;
+  int64_t ax;                                                // last acceptable iterate (x)
   int64_t total;
 };
 
@@ -89,14 +113,14 @@ struct Shape {
 };
 
 struct Result {            // per problem
-  int32_t status, iters, n_factor, pad;
+  int32_t status, iters, n_factor, n_resto;
   double objective, final_mu, nlp_error, sf;
   int64_t cyc[8];          // shader cycles: local sweeps, assembly, stage chain, kkt solves, total,
                            // errors+grad_lag, line search, update+re-eval
 };
 
 enum Status { ST_SUCCESS = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_RESTORATION = 3, ST_STEPFAIL = 4,
-              ST_BADINPUT = 5 };
+              ST_BADINPUT = 5, ST_CPUTIME = 6, ST_INFEASIBLE = 7, ST_TINYSTEP = 8 };
 
 HTP_HD inline void make_dims(Dims& d, int N, int M, int K, int topt, const int* eo, const int* eb) {
   d.N = N; d.M = M; d.K = K; d.topt = topt ? 1 : 0;
@@ -165,6 +189,15 @@ inline Layout make_layout(const Dims& d) {
   const int64_t nb2 = (int64_t)d.nb * d.nb;
   L.Kst = take(d.nblk * nb2); L.Off = take(d.nblk * nb2); L.LD = take(d.nblk * nb2); L.fac = take(d.nblk * nb2);
   L.V = take((int64_t)d.nblk * d.nb); L.X = take((int64_t)d.nblk * d.nb); L.ipiv = take((int64_t)d.nblk * d.nb);
+  const int64_t nR = 2 * (int64_t)d.mc + 2 * (int64_t)d.md, mcd = (int64_t)d.mc + d.md;
+  L.R = take(nR); L.Rt = take(nR); L.dR = take(nR); L.zR = take(nR); L.dzR = take(nR); L.eR = take(mcd);
+  L.rcf = take(d.mc); L.rdf = take(d.md); L.xR = take(d.n); L.dr = take(d.n); L.rRx = take(nR);
+  L.ox = take(d.n); L.os = take(d.md); L.oyc = take(d.mc); L.oyd = take(d.md); L.ozL = take(d.n); L.ozU = take(d.n);
+  L.ovL = take(d.md); L.ovU = take(d.md); L.ofilt = take(2 * 64); L.osv = take(64);
+  L.wx = take(d.n); L.ws = take(d.md); L.wyc = take(d.mc); L.wyd = take(d.md); L.wzL = take(d.n); L.wzU = take(d.n);
+  L.wvL = take(d.md); L.wvU = take(d.md); L.wR = take(nR); L.wzR = take(nR); L.wc = take(d.mc); L.wd = take(d.md);
+  L.wdx = take(d.n); L.wds = take(d.md); L.wdyc = take(d.mc); L.wdyd = take(d.md); L.wdR = take(nR);
+  L.ax = take(d.n);
   L.total = o;
   return L;
 }

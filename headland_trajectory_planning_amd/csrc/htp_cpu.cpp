@@ -21,7 +21,9 @@ extern "C" int htp_cpu_obca_solve_range(const htp_obca_batch* in, htp_obca_resul
                                         int64_t count, int nthreads) {
   const char* e = nullptr;
   if (check_shape(in, &e) || first < 0 || first + count > in->batch) return -1;
-  const Options o = default_options();
+  Options o = default_options();
+  o.wall_rate = 1e9;
+  o.wall_rate = 1e9;
   Dims D;
   make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
   const Layout L = make_layout(D);
@@ -49,6 +51,7 @@ extern "C" int htp_cpu_obca_solve_range(const htp_obca_batch* in, htp_obca_resul
       if (out->iterations) out->iterations[p] = r.iters;
       if (out->n_factor) out->n_factor[p] = r.n_factor;
       if (out->nlp_error) out->nlp_error[p] = r.nlp_error;
+      if (out->n_resto) out->n_resto[p] = r.n_resto;
     }
   }
   return 0;

@@ -12,6 +12,7 @@ struct htp_ctx {
   int device = 0;
   std::string err;
   Options opt = htp::default_options();
+  double wall_rate = 1e8;   // device wall-clock ticks/s (hipDeviceAttributeWallClockRate)
   void* ws = nullptr;
   size_t ws_bytes = 0;
   void* scratch = nullptr;  // Result array

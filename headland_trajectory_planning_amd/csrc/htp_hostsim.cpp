@@ -15,6 +15,7 @@ extern "C" int htp_hostsim_obca_solve(const htp_obca_batch* in, htp_obca_result*
   const char* e = nullptr;
   if (check_shape(in, &e)) return -1;
   Options o = default_options();
+  o.wall_rate = 1e9;
   for (int k = 0; k < nopt; ++k)
     if (set_option(o, names[k], values[k])) return -2;
   Dims D;
@@ -39,6 +40,7 @@ extern "C" int htp_hostsim_obca_solve(const htp_obca_batch* in, htp_obca_result*
     if (out->iterations) out->iterations[p] = r.iters;
     if (out->n_factor) out->n_factor[p] = r.n_factor;
     if (out->nlp_error) out->nlp_error[p] = r.nlp_error;
+      if (out->n_resto) out->n_resto[p] = r.n_resto;
   }
   return 0;
 }
@@ -48,6 +50,7 @@ extern "C" int htp_hostsim_obca_solve(const htp_obca_batch* in, htp_obca_result*
 extern "C" double htp_hostsim_debug_ws(const htp_obca_batch* in, int mode, double dw, double* ws_out,
                                        int64_t ws_len, int* neg_out) {
   Options o = default_options();
+  o.wall_rate = 1e9;
   Dims D;
   make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
   Layout L = make_layout(D);
@@ -76,6 +79,7 @@ extern "C" int htp_hostsim_obca_points_solve(const htp_obca_points_batch* in, ht
   const char* e = nullptr;
   if (check_shape_points(in, &e)) return -1;
   Options o = default_options();
+  o.wall_rate = 1e9;
   for (int k = 0; k < nopt; ++k)
     if (set_option(o, names[k], values[k])) return -2;
   Dims D;
@@ -99,6 +103,7 @@ extern "C" int htp_hostsim_obca_points_solve(const htp_obca_points_batch* in, ht
     if (out->iterations) out->iterations[p] = r.iters;
     if (out->n_factor) out->n_factor[p] = r.n_factor;
     if (out->nlp_error) out->nlp_error[p] = r.nlp_error;
+      if (out->n_resto) out->n_resto[p] = r.n_resto;
   }
   return 0;
 }

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(64, HTP_WAVES_PER_EU) void obca_points_kernel(const
 }
 
 __global__ void unpack_results(const Result* __restrict__ r, int batch, double* obj, int32_t* st, int32_t* it,
-                               int32_t* nf, double* err) {
+                               int32_t* nf, double* err, int32_t* nrs) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= batch) return;
   if (obj) obj[p] = r[p].objective;
@@ -96,6 +96,7 @@ __global__ void unpack_results(const Result* __restrict__ r, int batch, double* 
   if (it) it[p] = r[p].iters;
   if (nf) nf[p] = r[p].n_factor;
   if (err) err[p] = r[p].nlp_error;
+  if (nrs) nrs[p] = r[p].n_resto;
 }
 
 }  // namespace
@@ -124,6 +125,9 @@ htp_ctx* htp_create(int32_t device) {
     c->err = "hipSetDevice failed";
     return c;
   }
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+    c->wall_rate = 1e3 * (double)khz;
   (void)hipEventCreate(&c->ev0);
   (void)hipEventCreate(&c->ev1);
   (void)hipEventCreate(&c->rs_ev0);
@@ -200,6 +204,7 @@ int htp_obca_solve_batch_device(htp_ctx* ctx, const htp_obca_batch* in, htp_obca
   if (ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, sizeof(Result) * (size_t)in->batch)) return -1;
   if (!ctx->shape) HIPCHK(hipMalloc((void**)&ctx->shape, sizeof(Shape)));
   Shape hs{D, L, ctx->opt};
+  hs.o.wall_rate = ctx->wall_rate;
   BatchView b{in->traj, in->obs_A, in->obs_b, in->body_G, in->body_g, in->params,
               in->init_control, in->init_mu, in->init_lambda};
   hipStream_t s = (hipStream_t)stream;
@@ -223,7 +228,8 @@ int htp_obca_solve_batch_device(htp_ctx* ctx, const htp_obca_batch* in, htp_obca
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1, s));
   hipLaunchKernelGGL(unpack_results, dim3((in->batch + 255) / 256), dim3(256), 0, s, (const Result*)ctx->scratch,
-                     in->batch, out->objective, out->status, out->iterations, out->n_factor, out->nlp_error);
+                     in->batch, out->objective, out->status, out->iterations, out->n_factor, out->nlp_error,
+                     out->n_resto);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -245,7 +251,7 @@ int htp_obca_solve_batch(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result
   const size_t sz_la = in->init_lambda ? bytes(B * D.N * D.lam_count) : 0;
   const size_t sz_x = bytes(B * D.n);
   std::vector<size_t> sizes = {sz_traj, sz_A, sz_b, sz_G, sz_g, sz_p, sz_u, sz_mu, sz_la, sz_x,
-                               bytes(B), (size_t)B * 4, (size_t)B * 4, (size_t)B * 4, bytes(B)};
+                               bytes(B), (size_t)B * 4, (size_t)B * 4, (size_t)B * 4, bytes(B), (size_t)B * 4};
   size_t total = 0;
   std::vector<size_t> off;
   for (size_t s : sizes) { off.push_back(total); total += (s + 255) & ~size_t(255); }
@@ -275,6 +281,7 @@ int htp_obca_solve_batch(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result
   dout.iterations = (int32_t*)(dev + off[12]);
   dout.n_factor = (int32_t*)(dev + off[13]);
   dout.nlp_error = (double*)(dev + off[14]);
+  dout.n_resto = (int32_t*)(dev + off[15]);
   int rc = htp_obca_solve_batch_device(ctx, &din, &dout, nullptr);
   if (rc == 0) {
     hipError_t er = hipDeviceSynchronize();
@@ -283,9 +290,10 @@ int htp_obca_solve_batch(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result
   if (rc == 0) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) == hipSuccess) ctx->last_ms = ms;
-    struct { void* dst; size_t off, sz; } outs[6] = {{out->x, off[9], sz_x}, {out->objective, off[10], bytes(B)},
+    struct { void* dst; size_t off, sz; } outs[7] = {{out->x, off[9], sz_x}, {out->objective, off[10], bytes(B)},
                                                      {out->status, off[11], (size_t)B * 4}, {out->iterations, off[12], (size_t)B * 4},
-                                                     {out->n_factor, off[13], (size_t)B * 4}, {out->nlp_error, off[14], bytes(B)}};
+                                                     {out->n_factor, off[13], (size_t)B * 4}, {out->nlp_error, off[14], bytes(B)},
+                                                     {out->n_resto, off[15], (size_t)B * 4}};
     for (auto& o : outs)
       if (o.dst && hipMemcpy(o.dst, dev + o.off, o.sz, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(ctx, "copy back");
   }
@@ -320,6 +328,7 @@ int htp_obca_points_solve_batch_device(htp_ctx* ctx, const htp_obca_points_batch
   if (ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, sizeof(Result) * (size_t)in->batch)) return -1;
   if (!ctx->shape) HIPCHK(hipMalloc((void**)&ctx->shape, sizeof(Shape)));
   Shape hs{D, L, ctx->opt};
+  hs.o.wall_rate = ctx->wall_rate;
   const BatchView b = points_view(in);
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipMemcpyAsync(ctx->shape, &hs, sizeof(Shape), hipMemcpyHostToDevice, s));
@@ -335,7 +344,8 @@ int htp_obca_points_solve_batch_device(htp_ctx* ctx, const htp_obca_points_batch
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1, s));
   hipLaunchKernelGGL(unpack_results, dim3((in->batch + 255) / 256), dim3(256), 0, s, (const Result*)ctx->scratch,
-                     in->batch, out->objective, out->status, out->iterations, out->n_factor, out->nlp_error);
+                     in->batch, out->objective, out->status, out->iterations, out->n_factor, out->nlp_error,
+                     out->n_resto);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -355,7 +365,7 @@ int htp_obca_points_solve_batch(htp_ctx* ctx, const htp_obca_points_batch* in, h
   const void* srcs[6] = {in->traj, in->obs_A, in->obs_b, in->vertices, in->params, in->init_control};
   const size_t sz_x = bytes(B * D.n);
   std::vector<size_t> sizes(sz_in, sz_in + 6);
-  for (size_t v : {sz_x, bytes(B), (size_t)B * 4, (size_t)B * 4, (size_t)B * 4, bytes(B)}) sizes.push_back(v);
+  for (size_t v : {sz_x, bytes(B), (size_t)B * 4, (size_t)B * 4, (size_t)B * 4, bytes(B), (size_t)B * 4}) sizes.push_back(v);
   size_t total = 0;
   std::vector<size_t> off;
   for (size_t v : sizes) { off.push_back(total); total += (v + 255) & ~size_t(255); }
@@ -380,6 +390,7 @@ int htp_obca_points_solve_batch(htp_ctx* ctx, const htp_obca_points_batch* in, h
   dout.iterations = (int32_t*)(dev + off[9]);
   dout.n_factor = (int32_t*)(dev + off[10]);
   dout.nlp_error = (double*)(dev + off[11]);
+  dout.n_resto = (int32_t*)(dev + off[12]);
   int rc = htp_obca_points_solve_batch_device(ctx, &din, &dout, nullptr);
   if (rc == 0) {
     hipError_t er = hipDeviceSynchronize();
@@ -388,9 +399,10 @@ int htp_obca_points_solve_batch(htp_ctx* ctx, const htp_obca_points_batch* in, h
   if (rc == 0) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) == hipSuccess) ctx->last_ms = ms;
-    struct { void* dst; size_t off, sz; } outs[6] = {{out->x, off[6], sz_x}, {out->objective, off[7], bytes(B)},
+    struct { void* dst; size_t off, sz; } outs[7] = {{out->x, off[6], sz_x}, {out->objective, off[7], bytes(B)},
                                                      {out->status, off[8], (size_t)B * 4}, {out->iterations, off[9], (size_t)B * 4},
-                                                     {out->n_factor, off[10], (size_t)B * 4}, {out->nlp_error, off[11], bytes(B)}};
+                                                     {out->n_factor, off[10], (size_t)B * 4}, {out->nlp_error, off[11], bytes(B)},
+                                                     {out->n_resto, off[12], (size_t)B * 4}};
     for (auto& o : outs)
       if (o.dst && hipMemcpy(o.dst, dev + o.off, o.sz, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(ctx, "copy back");
   }

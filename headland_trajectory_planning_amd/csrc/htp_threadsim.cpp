@@ -60,6 +60,7 @@ struct ThreadWave {
     return s;
   }
   long long clock() const { return 0; }
+  long long wall() const { return 0; }
   double uniform(double v) const { return v; }
   int uniform_i(int v) const { return v; }
   double bcast(double v, int src) const {
@@ -103,6 +104,7 @@ extern "C" int htp_threadsim_obca_solve(const htp_obca_batch* in, htp_obca_resul
     if (out->iterations) out->iterations[p] = r.iters;
     if (out->n_factor) out->n_factor[p] = r.n_factor;
     if (out->nlp_error) out->nlp_error[p] = r.nlp_error;
+      if (out->n_resto) out->n_resto[p] = r.n_resto;
   }
   return 0;
 }

@@ -68,6 +68,11 @@ inline int set_option(Options& o, const char* name, double v) {
   HTP_OPT(delta) HTP_OPT(s_theta) HTP_OPT(s_phi) HTP_OPT(eta_phi) HTP_OPT(alpha_min_frac) HTP_OPT(kappa_soc)
   HTP_OPT(dw0) HTP_OPT(dw_min) HTP_OPT(dw_max) HTP_OPT(kw_minus) HTP_OPT(kw_plus) HTP_OPT(kw_plus_bar)
   HTP_OPT(dc_bar) HTP_OPT(kappa_c)
+  HTP_OPT(obj_max_inc) HTP_OPT(tiny_step_tol) HTP_OPT(tiny_step_y_tol) HTP_OPT(soft_resto_pderror_reduction_factor)
+  HTP_OPT(resto_penalty_parameter) HTP_OPT(resto_proximity_weight) HTP_OPT(required_infeasibility_reduction)
+  HTP_OPT(bound_mult_reset_threshold) HTP_OPT(max_filter_resets) HTP_OPT(filter_reset_trigger)
+  HTP_OPT(watchdog_shortened_iter_trigger) HTP_OPT(watchdog_trial_iter_max) HTP_OPT(max_soft_resto_iters)
+  HTP_OPT(max_cpu_time)
 #undef HTP_OPT
   return -1;
 }

@@ -309,6 +309,13 @@ struct ObcaSolver {
   double theta_min, theta_max;
   int n_factor;
   bool use_ric = false;
+  // restoration phase (oracle/ipm.py RestoProblem): the iterate is [x, R] with R = [n_c | p_c | n_d | p_d] >= 0,
+  // constraints c(x) + n_c - p_c = 0, d(x) + n_d - p_d - s = 0, objective rho sum R + eta/2 |D_R (x - x_R)|^2
+  bool rs = false;
+  double eta = 0.0;     // resto_proximity_weight * sqrt(mu) (restoration phase)
+  int nR = 0;           // 2 mc + 2 md
+  // objective factor of the Hessian: sf, or 0 in the restoration phase
+  HTP_HD HTP_FI double hsf() const { return rs ? 0.0 : sf; }
   long long cyc[8];
 #ifdef HTP_PROF_ON  // experiments: sub-step cycle counters of the stage chain (tools/build_variants.py)
   long long pcyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1013,6 +1020,23 @@ struct ObcaSolver {
     const double sa = scE[re], sb = scE[re + 1], s1 = scI[2 * p], s3 = scI[2 * p + 1];
     const double ya = sa * yc[re], yb = sb * yc[re + 1], y1 = s1 * yd[2 * p], y3 = s3 * yd[2 * p + 1];
     const double tx = x[NS * i], ty = x[NS * i + 1];
+    // restoration phase: rows carry the eliminated n/p diagonal, variables the proximity term
+    double ea = 0.0, eb = 0.0, e1 = 0.0, e3 = 0.0, prox[NZ];
+    for (int j = 0; j < NZ; ++j) prox[j] = 0.0;
+    if (rs) {
+      const gd* eR = A(L.eR);
+      ea = eR[re]; eb = eR[re + 1]; e1 = eR[D.mc + 2 * p]; e3 = eR[D.mc + 2 * p + 1];
+      if (!ls) {
+        const gd* dr = A(L.dr);
+        for (int j = 0; j < NZ; ++j) {
+          const bool is_mu = j < EN;
+          const int jj = is_mu ? j : j - EN;
+          const bool on = is_mu ? (jj < en) : (jj < em);
+          const int vi = is_mu ? mu0 + jj : la0 + jj;
+          prox[j] = on ? eta * dr[vi] * dr[vi] : 0.0;
+        }
+      }
+    }
     // inequality slack elimination
     if (ls) {
       B.Ds1 = 1.0;
@@ -1021,8 +1045,8 @@ struct ObcaSolver {
       B.Ds1 = vL1 / (sv1 - dL1) + vU1 / (dU1 - sv1) + dw;
       B.Ds3 = vL3 / (sv3 - dL3) + dw;
     }
-    B.E1 = 1.0 / B.Ds1 + dc;
-    B.E3 = 1.0 / B.Ds3 + dc;
+    B.E1 = 1.0 / B.Ds1 + dc + e1;
+    B.E3 = 1.0 / B.Ds3 + dc + e3;
     // Jacobian rows (z ordering: mu[0..EN), lam[0..EM)); padded entries are 0
     double Aw[EM], Atb[EM], A0[EM], A1[EM];
     for (int j = 0; j < EM; ++j) {
@@ -1068,7 +1092,7 @@ struct ObcaSolver {
       } else if (ls) {
         dg = 1.0;
       } else {
-        dg = zq[j] / (xq[j] - xlq[j]) + dw;
+        dg = zq[j] / (xq[j] - xlq[j]) + dw + prox[j];
       }
       B.K[B.pk(j, j)] += dg;
     }
@@ -1086,9 +1110,9 @@ struct ObcaSolver {
       B.K[B.pk(NZ, EN + j)] = sa * (cs * A0[j] + sn * A1[j]);
       B.K[B.pk(NZ + 1, EN + j)] = sb * (-sn * A0[j] + cs * A1[j]);
     }
-    B.K[B.pk(NZ, NZ)] = -dc;
+    B.K[B.pk(NZ, NZ)] = -(dc + ea);
     B.K[B.pk(NZ + 1, NZ)] = 0.0;
-    B.K[B.pk(NZ + 1, NZ + 1)] = -dc;
+    B.K[B.pk(NZ + 1, NZ + 1)] = -(dc + eb);
     // coupling B = [Hbar_zp; Cp]
     const double dRa = -sn * ya - cs * yb, dRb = cs * ya - sn * yb;  // dR^T/dth' y2
     for (int r = 0; r < NZ; ++r) {
@@ -1312,6 +1336,11 @@ struct ObcaSolver {
     }
     E1 = 1.0 / Ds1 + dc;
     E3 = 1.0 / Ds3 + dc;
+    if (rs) {
+      const gd* eR = A(L.eR);
+      E1 += eR[D.mc + r1];
+      E3 += eR[D.mc + r3];
+    }
   }
   // scaled Jacobian rows of block p, vertex k: J1 = s1 2 A w (z only), J3 = [J3z | J3p]
   HTP_HD HTP_FI void pt_row_jac(const PtGeom& G, int p, int k, double& s1, double* J3z, double* J3p, double* dv,
@@ -1376,6 +1405,7 @@ struct ObcaSolver {
       } else {
         const int vi = G.la0 + j;
         dg = zL[vi] / (x[vi] - xL[vi]) + zU[vi] / (xU[vi] - x[vi]) + dw;
+        if (rs) dg += eta * A(L.dr)[vi] * A(L.dr)[vi];
       }
       B.K[B.pk(j, j)] += dg;
     }
@@ -1526,11 +1556,27 @@ struct ObcaSolver {
     const gd* scE = A(L.scE);
     gd* K = A(L.Kst) + (int64_t)N * nb * nb;
     gd* O = A(L.Off) + (int64_t)N * nb * nb;
+    const gd* eR = A(L.eR);
     for (int q = c.lane; q < nb * nb; q += c.width) {
       const int r = q / nb, cc = q % nb;
-      K[q] = (r == cc) ? (r < NS ? -dc : 1.0) : 0.0;
+      K[q] = (r == cc) ? (r < NS ? -(dc + (rs ? eR[D.eTerm + r] : 0.0)) : 1.0) : 0.0;
       O[q] = (r < NS && cc == NS + r) ? scE[D.eTerm + r] : 0.0;
     }
+  }
+
+  // terminal slack s_k (free, objective 5000 s_k^2): Hs = 10000 sf + dw (+ eta D_R^2 in the restoration phase),
+  // and the eliminated terminal row's Et = dc (+ eR) + st^2 / Hs
+  HTP_HD HTP_FI double term_H(int k, bool ls, double dw) const {
+    if (ls) return 1.0;
+    double h = 10000.0 * hsf() + dw;
+    if (rs) h += eta * A(L.dr)[D.oS + k] * A(L.dr)[D.oS + k];
+    return h;
+  }
+  HTP_HD HTP_FI double term_E(int k, bool ls, double dw, double dc) const {
+    const double st = A(L.scE)[D.eTerm + k];
+    double e = dc + st * st / term_H(k, ls, dw);
+    if (rs) e += A(L.eR)[D.eTerm + k];
+    return e;
   }
 
   HTP_HD HTP_FI bool uniform44() const {
@@ -1583,14 +1629,23 @@ struct ObcaSolver {
       xq[a] = x[q]; xlq[a] = xL[q]; xuq[a] = xU[q]; zlq[a] = zL[q]; zuq[a] = zU[q];
     }
     for (int k = 0; k < NS; ++k) sce[k] = scE[rowbase + k];
-    for (int k = 0; k < NS; ++k) add(k, k, -dc);
+    double er[NS] = {0.0, 0.0, 0.0, 0.0, 0.0}, pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (rs) {
+      const gd* eR = A(L.eR);
+      const gd* dr = A(L.dr);
+      for (int k = 0; k < NS; ++k) er[k] = eR[rowbase + k];
+      if (!ls)
+        for (int a = 0; a < 8; ++a) pr[a] = eta * dr[vidx[a]] * dr[vidx[a]];
+    }
+    const double hs = hsf();
+    for (int k = 0; k < NS; ++k) add(k, k, -(dc + er[k]));
     for (int k = 0; k < NS; ++k) add(k, NS + k, sce[k]);
     for (int a = 0; a < 8; ++a) {
       if (a < nv) {
         double dg;
         if (ls) dg = 1.0;
         else {
-          dg = dw;
+          dg = dw + pr[a];
           if (finite_(xlq[a])) dg += zlq[a] / (xq[a] - xlq[a]);
           if (finite_(xuq[a])) dg += zuq[a] / (xuq[a] - xq[a]);
         }
@@ -1601,14 +1656,14 @@ struct ObcaSolver {
       if (a >= nv && a < D.nw) add(NS + a, NS + a, 1.0);  // padding (last stage)
     if (PT && !ls && i < N - 1) {  // optimizer_points.py objective: 20 (v dT)^2, (u_{i+1} - u_i)^2
       const int U0 = NS + 5, V0 = NS + 2;
-      add(V0, V0, sf * 40.0 * dT * dT);
+      add(V0, V0, hs * 40.0 * dT * dT);
       if (i < N - 2) {
-        add(U0, U0, sf * 2.0);
-        add(U0 + 1, U0 + 1, sf * 2.0);
+        add(U0, U0, hs * 2.0);
+        add(U0 + 1, U0 + 1, hs * 2.0);
       }
       if (i >= 1) {
-        add(U0, U0, sf * 2.0);
-        add(U0 + 1, U0 + 1, sf * 2.0);
+        add(U0, U0, hs * 2.0);
+        add(U0 + 1, U0 + 1, hs * 2.0);
       }
     }
     if (!ls && i < N - 1) {
@@ -1617,35 +1672,35 @@ struct ObcaSolver {
       const double Qs00 = 2 * par(P_Q00), Qs01 = par(P_Q01) + par(P_Q10), Qs11 = 2 * par(P_Q11);
       const double Rs00 = 2 * par(P_R00), Rs01 = par(P_R01) + par(P_R10), Rs11 = 2 * par(P_R11);
       const int U0 = NS + 5, T0 = NS + 7, V0 = NS + 2;
-      add(U0, U0, sf * Qs00);
-      add(U0 + 1, U0, sf * Qs01);
-      add(U0 + 1, U0 + 1, sf * Qs11);
+      add(U0, U0, hs * Qs00);
+      add(U0 + 1, U0, hs * Qs01);
+      add(U0 + 1, U0 + 1, hs * Qs11);
       const double v = x[NS * i + 2];
-      add(V0, V0, sf * 2.0 * par(P_W00) * h * h);
+      add(V0, V0, hs * 2.0 * par(P_W00) * h * h);
       if (D.topt) {
-        add(T0, T0, sf * 2.0 * par(P_W00) * v * v * dT * dT);
-        add(V0, T0, sf * 4.0 * par(P_W00) * v * dT * dT * tau);
+        add(T0, T0, hs * 2.0 * par(P_W00) * v * v * dT * dT);
+        add(V0, T0, hs * 4.0 * par(P_W00) * v * dT * dT * tau);
       }
       if (i < N - 2) {
         const double ih2 = 1.0 / (h * h);
-        add(U0, U0, sf * Rs00 * ih2);
-        add(U0 + 1, U0, sf * Rs01 * ih2);
-        add(U0 + 1, U0 + 1, sf * Rs11 * ih2);
+        add(U0, U0, hs * Rs00 * ih2);
+        add(U0 + 1, U0, hs * Rs01 * ih2);
+        add(U0 + 1, U0 + 1, hs * Rs11 * ih2);
         if (D.topt) {
           const double da = x[D.oU + NC * (i + 1)] - x[D.oU + NC * i];
           const double dw_ = x[D.oU + NC * (i + 1) + 1] - x[D.oU + NC * i + 1];
           const double Jv = (da * (par(P_R00) * da + par(P_R01) * dw_) + dw_ * (par(P_R10) * da + par(P_R11) * dw_)) * ih2;
-          add(T0, T0, sf * 6.0 * Jv / (tau * tau));
+          add(T0, T0, hs * 6.0 * Jv / (tau * tau));
           const double k2 = 2.0 * ih2 / tau;
-          add(U0, T0, sf * k2 * (Rs00 * da + Rs01 * dw_));
-          add(U0 + 1, T0, sf * k2 * (Rs01 * da + Rs11 * dw_));
+          add(U0, T0, hs * k2 * (Rs00 * da + Rs01 * dw_));
+          add(U0 + 1, T0, hs * k2 * (Rs01 * da + Rs11 * dw_));
         }
       }
       if (i >= 1 && i - 1 < N - 2) {  // jerk_{i-1} on (u_i,u_i)
         const double hp = dT * tauv(x, i - 1), ih2 = 1.0 / (hp * hp);
-        add(U0, U0, sf * Rs00 * ih2);
-        add(U0 + 1, U0, sf * Rs01 * ih2);
-        add(U0 + 1, U0 + 1, sf * Rs11 * ih2);
+        add(U0, U0, hs * Rs00 * ih2);
+        add(U0 + 1, U0, hs * Rs01 * ih2);
+        add(U0 + 1, U0 + 1, hs * Rs11 * ih2);
       }
       }
       // dynamics Hessian of interval i:  sum_k (-yhat_k) d2F_k
@@ -1670,12 +1725,11 @@ struct ObcaSolver {
       add(NS + 3, NS + 1, S[4]);
       add(NS + 3, NS + 3, S[5]);
     }
-    // terminal slack block (i == N-1): Hs = 10000 sf + dw
+    // terminal slack block (i == N-1): Hs = 10000 sf + dw (+ proximity), Et = dc (+ eR) + st^2 / Hs
     if (!PT && i == N - 1) {
-      const double Hs = ls ? 1.0 : 10000.0 * sf + dw;
       for (int k = 0; k < NS; ++k) {
         const double st = scE[D.eTerm + k];
-        const double Et = dc + st * st / Hs;
+        const double Et = term_E(k, ls, dw, dc);
         add(NS + k, NS + k, st * st / Et);
       }
     }
@@ -1703,23 +1757,23 @@ struct ObcaSolver {
       }
       if (PT && !ls && i < N - 2) {
         const int U0 = NS + 5;
-        O[U0 * nb + U0] = -sf * 2.0;
-        O[(U0 + 1) * nb + U0 + 1] = -sf * 2.0;
+        O[U0 * nb + U0] = -hs * 2.0;
+        O[(U0 + 1) * nb + U0 + 1] = -hs * 2.0;
       }
       if (!PT && !ls && i < N - 2) {
         const double tau = tauv(x, i), h = dT * tau, ih2 = 1.0 / (h * h);
         const double Rs00 = 2 * par(P_R00), Rs01 = par(P_R01) + par(P_R10), Rs11 = 2 * par(P_R11);
         const int U0 = NS + 5, T0 = NS + 7;
-        O[U0 * nb + U0] = -sf * Rs00 * ih2;
-        O[U0 * nb + U0 + 1] = -sf * Rs01 * ih2;
-        O[(U0 + 1) * nb + U0] = -sf * Rs01 * ih2;
-        O[(U0 + 1) * nb + U0 + 1] = -sf * Rs11 * ih2;
+        O[U0 * nb + U0] = -hs * Rs00 * ih2;
+        O[U0 * nb + U0 + 1] = -hs * Rs01 * ih2;
+        O[(U0 + 1) * nb + U0] = -hs * Rs01 * ih2;
+        O[(U0 + 1) * nb + U0 + 1] = -hs * Rs11 * ih2;
         if (D.topt) {
           const double da = x[D.oU + NC * (i + 1)] - x[D.oU + NC * i];
           const double dw_ = x[D.oU + NC * (i + 1) + 1] - x[D.oU + NC * i + 1];
           const double k2 = -2.0 * ih2 / tau;
-          O[U0 * nb + T0] = sf * k2 * (Rs00 * da + Rs01 * dw_);
-          O[(U0 + 1) * nb + T0] = sf * k2 * (Rs01 * da + Rs11 * dw_);
+          O[U0 * nb + T0] = hs * k2 * (Rs00 * da + Rs01 * dw_);
+          O[(U0 + 1) * nb + T0] = hs * k2 * (Rs01 * da + Rs11 * dw_);
         }
       }
     }
@@ -2340,6 +2394,7 @@ struct ObcaSolver {
     const int N = D.N, nb = D.nb;
     int neg = 0, zero = 0;
     long long t0 = c.clock();
+    if (rs) compute_eR(ls, dw);
     local_factor_sweep<EN_, EM_>(ls, dw, dc, neg, zero);
     neg = c.isum(neg);
     zero = c.isum(zero);
@@ -2370,7 +2425,7 @@ struct ObcaSolver {
     long long t2 = c.clock();
     cyc[1] += t2 - t1;
     // (the point formulation's hard terminal rows have no Riccati form: block LDL^T)
-    if (!PT && dc == 0.0) {
+    if (!PT && dc == 0.0 && !rs) {
       const int bad = riccati_factor();
       use_ric = true;
       cyc[2] += c.clock() - t2;
@@ -2431,17 +2486,48 @@ struct ObcaSolver {
   }
 
   // solve K [ox; os; oc; od] = [bx; bs; bc; bd] with the current factorization
+  // Restoration phase: the n/p rows (S_n + dw) dn + dy = b_n, (S_p + dw) dp - dy = b_p are eliminated onto the
+  // constraint rows (eR = 1/(S_n+dw) + 1/(S_p+dw) on the diagonal), b_c -> b_c - b_n/(S_n+dw) + b_p/(S_p+dw).
+  HTP_HD HTP_FI void np_diag(int j, bool ls, double dw, double& sn, double& sp) const {
+    const gd* R = A(L.R); const gd* zR = A(L.zR);
+    const int jp = j < D.mc ? j + D.mc : j + D.md;   // n index j -> its p index
+    sn = ls ? 1.0 : zR[j] / R[j] + dw;
+    sp = ls ? 1.0 : zR[jp] / R[jp] + dw;
+  }
+  HTP_HD HTP_FI void compute_eR(bool ls, double dw) {
+    gd* eR = A(L.eR);
+    for (int r = c.lane; r < D.mc + D.md; r += c.width) {
+      const int j = r < D.mc ? r : r + D.mc;       // n index of row r
+      double sn, sp;
+      np_diag(j, ls, dw, sn, sp);
+      eR[r] = 1.0 / sn + 1.0 / sp;
+    }
+    c.sync();
+  }
+
   HTP_HD HTP_PHASE void kkt_solve(bool ls, double dw, double dc, const gd* bx, const gd* bs, const gd* bc,
-                        const gd* bd, gd* ox, gd* os, gd* oc, gd* od) {
+                        const gd* bd, gd* ox, gd* os, gd* oc, gd* od, const gd* bR = nullptr, gd* oR = nullptr) {
     const int N = D.N, nb = D.nb;
     const long long t0 = c.clock();
+    if (rs) {  // fold the n/p right-hand sides into the constraint rows
+      gd* fc = A(L.rcf); gd* fd = A(L.rdf);
+      for (int r = c.lane; r < D.mc + D.md; r += c.width) {
+        const int j = r < D.mc ? r : r + D.mc, jp = r < D.mc ? r + D.mc : r + D.mc + D.md;
+        double sn, sp;
+        np_diag(j, ls, dw, sn, sp);
+        if (r < D.mc) fc[r] = bc[r] - bR[j] / sn + bR[jp] / sp;
+        else fd[r - D.mc] = bd[r - D.mc] - bR[j] / sn + bR[jp] / sp;
+      }
+      c.sync();
+      bc = fc;
+      bd = fd;
+    }
     local_rhs_sweep<EN_, EM_>(ls, dw, dc, bx, bs, bc, bd);
     c.sync();
     const gd* PR = A(L.pairR);
     const gd* scE = A(L.scE);
     gd* V = A(L.V);
     const int MK = blocks_per_stage();
-    const double Hs = ls ? 1.0 : 10000.0 * sf + dw;
     for (int i = c.lane; i < N; i += c.width) {
       // the stage rhs is built in registers and stored once (no read-modify-write in HBM)
       gd* r = V + (int64_t)i * nb;
@@ -2458,7 +2544,7 @@ struct ObcaSolver {
         if constexpr (!PT)
           for (int k = 0; k < NS; ++k) {
             const double st = scE[D.eTerm + k];
-            const double Et = dc + st * st / Hs;
+            const double Hs = term_H(k, ls, dw), Et = term_E(k, ls, dw, dc);
             rv[NS + k] -= st / Et * (st * bx[D.oS + k] / Hs - bc[D.eTerm + k]);
           }
       }
@@ -2529,7 +2615,7 @@ struct ObcaSolver {
       } else {
         for (int k = 0; k < NS; ++k) {
           const double st = scE[D.eTerm + k];
-          const double Et = dc + st * st / Hs;
+          const double Hs = term_H(k, ls, dw), Et = term_E(k, ls, dw, dc);
           const double yt = (st * xi[NS + k] + st * bx[D.oS + k] / Hs - bc[D.eTerm + k]) / Et;
           oc[D.eTerm + k] = yt;
           ox[D.oS + k] = (bx[D.oS + k] - st * yt) / Hs;
@@ -2539,10 +2625,22 @@ struct ObcaSolver {
     c.sync();
     local_back_sweep<EN_, EM_>(ls, dw, dc, bx, bs, bc, bd, ox, os, oc, od);
     c.sync();
+    if (rs) {  // dn = (b_n - dy) / (S_n + dw), dp = (b_p + dy) / (S_p + dw)
+      for (int r = c.lane; r < D.mc + D.md; r += c.width) {
+        const int j = r < D.mc ? r : r + D.mc, jp = r < D.mc ? r + D.mc : r + D.mc + D.md;
+        double sn, sp;
+        np_diag(j, ls, dw, sn, sp);
+        const double dy = r < D.mc ? oc[r] : od[r - D.mc];
+        oR[j] = (bR[j] - dy) / sn;
+        oR[jp] = (bR[jp] + dy) / sp;
+      }
+      c.sync();
+    }
     cyc[3] += c.clock() - t0;
   }
   // ======================================================== IPM driver
-  // Mirrors oracle/ipm.py IpoptRestatement.solve line by line.
+  // Mirrors oracle/ipm.py (_Ipm.run, find_trial, backtrack, second_order_correction,
+  // try_soft_resto_step, restoration, resto_check, resto_resto) decision by decision.
   int nbL, nbU, nsL, nsU;  // counts of finite bounds
 
   HTP_HD HTP_FI void count_bounds() {
@@ -2565,14 +2663,23 @@ struct ObcaSolver {
 
   struct Err { double dual, comp, s_d, s_c, prim_b, prim_nlp; };
 
-  // grad Lagrangian (x part, w/o bound multipliers) -> rx
-  HTP_HD HTP_FI void grad_lag_into(gd* out) {
-    eval_jt(A(L.x), A(L.yc), A(L.yd), out);
-    const gd* gf = A(L.gf);
+  // J_R' y entry of restoration variable j (n: +y, p: -y)
+  HTP_HD HTP_FI double np_jty(int j, const gd* yc, const gd* yd) const {
+    const int mc = D.mc, md = D.md;
+    if (j < mc) return yc[j];
+    if (j < 2 * mc) return -yc[j - mc];
+    if (j < 2 * mc + md) return yd[j - 2 * mc];
+    return -yd[j - 2 * mc - md];
+  }
+
+  // grad Lagrangian (x part, w/o bound multipliers) at (x, yc, yd) -> out; gf must hold grad f at x
+  HTP_HD HTP_FI void grad_lag_at(const gd* x, const gd* yc, const gd* yd, const gd* gf, gd* out) {
+    eval_jt(x, yc, yd, out);
     double a_[SW_U], b_[SW_U];
     sweep(D.n, [&](int q, int k) { a_[k] = out[q]; b_[k] = gf[q]; }, [&](int q, int k) { out[q] = a_[k] + b_[k]; });
     c.sync();
   }
+  HTP_HD HTP_FI void grad_lag_into(gd* out) { grad_lag_at(A(L.x), A(L.yc), A(L.yd), A(L.gf), out); }
 
   HTP_HD HTP_PHASE Err errors(const gd* gl, double mu_) const {
     const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
@@ -2615,6 +2722,15 @@ struct ObcaSolver {
               pn = dmax(pn, dabs(c_[k]));
             });
     }
+    if (rs) {  // n/p: rho + J_R'y - z_R, complementarity R z_R
+      const gd* R = A(L.R); const gd* zR = A(L.zR);
+      const double rho = o.resto_penalty_parameter;
+      for (int j = c.lane; j < nR; j += c.width) {
+        dual = dmax(dual, dabs(rho + np_jty(j, yc, yd) - zR[j]));
+        comp = dmax(comp, dabs(R[j] * zR[j] - mu_));
+        zsum += dabs(zR[j]);
+      }
+    }
     Err e;
     e.dual = c.maxv(dual);
     e.comp = c.maxv(comp);
@@ -2622,18 +2738,67 @@ struct ObcaSolver {
     ysum = c.sum(ysum);
     e.prim_b = c.maxv(pb);
     e.prim_nlp = c.maxv(pn);
-    const int nz = nbL + nbU + nsL + nsU, ny = D.mc + D.md;
+    const int nz = nbL + nbU + nsL + nsU + (rs ? nR : 0), ny = D.mc + D.md;
     e.s_d = dmax(o.s_max, (ysum + zsum) / (double)(ny + nz > 0 ? ny + nz : 1)) / o.s_max;
     e.s_c = dmax(o.s_max, zsum / (double)(nz > 0 ? nz : 1)) / o.s_max;
     return e;
   }
 
-  // unscaled constraint violation of the original NLP at x (uses c, d arrays)
+  // IPOPT curr_primal_dual_system_error(mu): averaged 1-norms of dual infeasibility, primal
+  // infeasibility and relaxed complementarity at the point given by the arrays
+  HTP_HD HTP_FI double pd_error(const gd* gl, const gd* x, const gd* s, const gd* yc, const gd* yd, const gd* zL,
+                                const gd* zU, const gd* vL, const gd* vU, const gd* R, const gd* zR, const gd* cc,
+                                const gd* dd, double mu_, bool safe = false) const {
+    const gd* xL = A(L.xL); const gd* xU = A(L.xU); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
+    const gd* czL = A(L.zL); const gd* czU = A(L.zU); const gd* cvL = A(L.vL); const gd* cvU = A(L.vU);
+    auto sl = [&](double v, double z, double b) { return safe ? safe_slack(v, z, b, mu_) : v; };
+    double du = 0, pr = 0, cs = 0;
+    int ncs = 0;
+    for (int q = c.lane; q < D.n; q += c.width) {
+      du += dabs(gl[q] - zL[q] + zU[q]);
+      if (finite_(xL[q])) { cs += dabs(sl(x[q] - xL[q], czL[q], xL[q]) * zL[q] - mu_); ++ncs; }
+      if (finite_(xU[q])) { cs += dabs(sl(xU[q] - x[q], czU[q], xU[q]) * zU[q] - mu_); ++ncs; }
+    }
+    for (int r = c.lane; r < D.md; r += c.width) {
+      du += dabs(-yd[r] - vL[r] + vU[r]);
+      pr += dabs(dd[r] - s[r]);
+      cs += dabs(sl(s[r] - dL[r], cvL[r], dL[r]) * vL[r] - mu_);
+      ++ncs;
+      if (finite_(dU[r])) { cs += dabs(sl(dU[r] - s[r], cvU[r], dU[r]) * vU[r] - mu_); ++ncs; }
+    }
+    for (int r = c.lane; r < D.mc; r += c.width) pr += dabs(cc[r]);
+    if (rs) {
+      const double rho = o.resto_penalty_parameter;
+      for (int j = c.lane; j < nR; j += c.width) {
+        du += dabs(rho + np_jty(j, yc, yd) - zR[j]);
+        cs += dabs(R[j] * zR[j] - mu_);
+        ++ncs;
+      }
+    }
+    du = c.sum(du);
+    pr = c.sum(pr);
+    cs = c.sum(cs);
+    ncs = c.isum(ncs);
+    const int ndual = D.n + D.md + (rs ? nR : 0), nprim = D.mc + D.md;
+    return du / (double)(ndual > 0 ? ndual : 1) + (nprim ? pr / (double)nprim : 0.0) + (ncs ? cs / (double)ncs : 0.0);
+  }
+
+  // unscaled constraint violation (original NLP at x: c, d arrays are scaled); the restoration
+  // problem is unscaled and its inequality bounds are the relaxed scaled ones
   HTP_HD HTP_FI double unscaled_viol() const {
     const gd* cc = A(L.c); const gd* dd = A(L.d);
     const gd* scE = A(L.scE); const gd* scI = A(L.scI);
     const double dmn = par(P_DMIN);
     double v = 0;
+    if (rs) {
+      const gd* dL = A(L.dL); const gd* dU = A(L.dU);
+      for (int r = c.lane; r < D.mc; r += c.width) v = dmax(v, dabs(cc[r]));
+      for (int r = c.lane; r < D.md; r += c.width) {
+        v = dmax(v, dL[r] - dd[r]);
+        if (finite_(dU[r])) v = dmax(v, dd[r] - dU[r]);
+      }
+      return c.maxv(v);
+    }
     {
       double c_[SW_U], e_[SW_U];
       sweep(D.mc, [&](int r, int k) { c_[k] = cc[r]; e_[k] = scE[r]; },
@@ -2665,41 +2830,88 @@ struct ObcaSolver {
     return c.sum(t);
   }
 
-  // barrier function; returns +inf (as 1e308*10) if a slack is not positive
-  HTP_HD HTP_PHASE double barrier(const gd* x, const gd* s, double mu_) const {
+  // original-problem theta at (x, s) during the restoration phase: c = c_R - n + p, d = d_R - n_d + p_d
+  HTP_HD HTP_FI double orig_theta_rs(const gd* cc, const gd* dd, const gd* s, const gd* R) const {
+    const int mc = D.mc, md = D.md;
+    double t = 0;
+    for (int r = c.lane; r < mc; r += c.width) t += dabs(cc[r] - R[r] + R[mc + r]);
+    for (int r = c.lane; r < md; r += c.width) t += dabs(dd[r] - R[2 * mc + r] + R[2 * mc + md + r] - s[r]);
+    return c.sum(t);
+  }
+
+  // barrier function at (x, s[, R]); +inf if a slack is not positive.  resto_obj: the restoration
+  // problem's objective and n/p barrier terms, else the original sf * f
+  HTP_HD HTP_PHASE double barrier(const gd* x, const gd* s, const gd* Rv, double mu_, bool resto_obj) const {
     const gd* xL = A(L.xL); const gd* xU = A(L.xU);
     const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     const double kd = o.kappa_d * mu_;
     double lg = 0.0, lin = 0.0;
     int bad = 0;
+    const gd* zL = A(L.zL); const gd* zU = A(L.zU); const gd* vL = A(L.vL); const gd* vU = A(L.vU);
     {
       double x_[SW_U], xl_[SW_U], xu_[SW_U];
       sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; },
-            [&](int, int k) {
+            [&](int q, int k) {
               const bool hl = finite_(xl_[k]), hu = finite_(xu_[k]);
-              if (hl) { const double v = x_[k] - xl_[k]; if (v <= 0) bad = 1; else lg += log(v); if (!hu) lin += v; }
-              if (hu) { const double v = xu_[k] - x_[k]; if (v <= 0) bad = 1; else lg += log(v); if (!hl) lin += v; }
+              if (hl) { const double v = safe_slack(x_[k] - xl_[k], zL[q], xl_[k], mu_); if (v <= 0) bad = 1; else lg += log(v); if (!hu) lin += v; }
+              if (hu) { const double v = safe_slack(xu_[k] - x_[k], zU[q], xu_[k], mu_); if (v <= 0) bad = 1; else lg += log(v); if (!hl) lin += v; }
             });
+    }
+    double fobj = 0.0;
+    if (resto_obj) {  // rho sum R + eta/2 |D_R (x - x_R)|^2 ; n/p barrier terms (lower bounds 0)
+      const gd* xR = A(L.xR); const gd* dr = A(L.dr);
+      const double et = o.resto_proximity_weight * sqrt(mu_);
+      double px = 0.0, sr = 0.0;
+      for (int q = c.lane; q < D.n; q += c.width) { const double t = dr[q] * (x[q] - xR[q]); px += t * t; }
+      for (int j = c.lane; j < nR; j += c.width) {
+        const double v = Rv[j];
+        if (v <= 0) bad = 1; else lg += log(v);
+        lin += v;
+        sr += v;
+      }
+      fobj = o.resto_penalty_parameter * c.sum(sr) + 0.5 * et * c.sum(px);
     }
     {
       double s_[SW_U], dl_[SW_U], du_[SW_U];
       sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = dU[r]; },
-            [&](int, int k) {
+            [&](int r, int k) {
               const bool hu = finite_(du_[k]);
-              const double v = s_[k] - dl_[k];
+              const double v = safe_slack(s_[k] - dl_[k], vL[r], dl_[k], mu_);
               if (v <= 0) bad = 1; else lg += log(v);
               if (!hu) lin += v;
-              if (hu) { const double w = du_[k] - s_[k]; if (w <= 0) bad = 1; else lg += log(w); }
+              if (hu) { const double w = safe_slack(du_[k] - s_[k], vU[r], du_[k], mu_); if (w <= 0) bad = 1; else lg += log(w); }
             });
     }
     bad = c.isum(bad);
     lg = c.sum(lg);
     lin = c.sum(lin);
     if (bad) return HTP_INF;
-    return sf * eval_f(x) - mu_ * lg + kd * lin;
+    if (!resto_obj) fobj = sf * eval_f(x);
+    return fobj - mu_ * lg + kd * lin;
   }
 
-  // barrier gradient -> gx (n), gs (md); needs gf current
+  // restoration objective gradient (x part): eta D_R^2 (x - x_R)
+  HTP_HD HTP_FI void eval_grad_f_rs(const gd* x, gd* g) const {
+    const gd* xR = A(L.xR); const gd* dr = A(L.dr);
+    for (int q = c.lane; q < D.n; q += c.width) g[q] = eta * dr[q] * dr[q] * (x[q] - xR[q]);
+    c.sync();
+  }
+  HTP_HD HTP_FI void eval_grad_mode(const gd* x) {
+    if (rs) eval_grad_f_rs(x, A(L.gf));
+    else eval_grad_f(x, A(L.gf), sf);
+  }
+  // constraint values of the current mode at (x[, R]) into (cc, dd)
+  HTP_HD HTP_FI void eval_cons_mode(const gd* x, const gd* Rv, gd* cc, gd* dd) const {
+    eval_cons(x, cc, dd);
+    if (rs) {
+      const int mc = D.mc, md = D.md;
+      for (int r = c.lane; r < mc; r += c.width) cc[r] += Rv[r] - Rv[mc + r];
+      for (int r = c.lane; r < md; r += c.width) dd[r] += Rv[2 * mc + r] - Rv[2 * mc + md + r];
+      c.sync();
+    }
+  }
+
+  // barrier gradient -> gx (n), gs (md); needs gf current (n/p part: rho - mu/R + kd, computed inline)
   HTP_HD HTP_FI void grad_barrier(double mu_, gd* gx, gd* gs) const {
     const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
     const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
@@ -2731,8 +2943,11 @@ struct ObcaSolver {
     }
     c.sync();
   }
+  HTP_HD HTP_FI double np_grad_barrier(int j, const gd* R, double mu_) const {
+    return o.resto_penalty_parameter - mu_ / R[j] + o.kappa_d * mu_;
+  }
 
-  HTP_HD HTP_FI double frac_primal(const gd* dx, const gd* ds) const {
+  HTP_HD HTP_FI double frac_primal(const gd* dx, const gd* ds, const gd* dR) const {
     const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
     const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     double a = 1.0;
@@ -2752,11 +2967,16 @@ struct ObcaSolver {
               if (finite_(du_[k]) && -d_[k] < 0) a = dmin(a, -tau * (du_[k] - s_[k]) / (-d_[k]));
             });
     }
+    if (rs) {
+      const gd* R = A(L.R);
+      for (int j = c.lane; j < nR; j += c.width)
+        if (dR[j] < 0) a = dmin(a, -tau * R[j] / dR[j]);
+    }
     return c.minv(a);
   }
 
-  // bound-multiplier steps for (dx, ds) -> dzL, dzU, dvL, dvU ; returns alpha_dual
-  HTP_HD HTP_FI double dual_steps(const gd* dx, const gd* ds) {
+  // bound-multiplier steps for (dx, ds[, dR]) -> dzL, dzU, dvL, dvU[, dzR] ; returns alpha_dual
+  HTP_HD HTP_FI double dual_steps(const gd* dx, const gd* ds, const gd* dR) {
     const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
     const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     const gd* zL = A(L.zL); const gd* zU = A(L.zU);
@@ -2787,8 +3007,26 @@ struct ObcaSolver {
               dvU[r] = u;
             });
     }
+    if (rs) {
+      const gd* R = A(L.R); const gd* zR = A(L.zR);
+      gd* dzR = A(L.dzR);
+      for (int j = c.lane; j < nR; j += c.width) {
+        const double t = (mu - zR[j] * R[j] - zR[j] * dR[j]) / R[j];
+        if (t < 0) a = dmin(a, -tau * zR[j] / t);
+        dzR[j] = t;
+      }
+    }
     c.sync();
     return c.minv(a);
+  }
+
+  // IpoptCalculatedQuantities::CalculateSafeSlack: a slack below eps * min(1, mu) becomes
+  // min(max(mu / z, s_min), max(slack, 0) + slack_move * max(1, |bound|)) (z: current multiplier)
+  static constexpr double SLACK_MOVE = 1.8189894035458565e-12;  // eps^(3/4)
+  HTP_HD HTP_FI static double safe_slack(double v, double z, double bound, double mu_) {
+    const double smin = 2.220446049250313e-16 * dmin(1.0, mu_);
+    if (!(v < smin)) return v;
+    return dmin(dmax(mu_ / z, smin), dmax(v, 0.0) + SLACK_MOVE * dmax(1.0, dabs(bound)));
   }
 
   HTP_HD HTP_FI static bool cmp_le(double lhs, double rhs, double basval) {
@@ -2815,22 +3053,131 @@ struct ObcaSolver {
     }
   }
 
-  // trial acceptability test (filter / Armijo); evaluates ct, dt at (xt, st)
-  HTP_HD HTP_PHASE bool acceptable(double a, const gd* xt, const gd* st, double phi, double theta, double gBD,
-                         bool ftype_ok, double& th_t, double& ph_t) {
-    gd* ct = A(L.ct);
-    gd* dtv = A(L.dt);
-    eval_cons(xt, ct, dtv);
-    th_t = theta_of(ct, dtv, st);
-    ph_t = barrier(xt, st, mu);
-    if (!(ph_t < 1e300) || th_t > theta_max) return false;
-    bool ok;
-    if (a > 0 && ftype_ok && theta <= theta_min) ok = cmp_le(ph_t - phi, o.eta_phi * a * gBD, phi);
-    else ok = cmp_le(th_t, (1 - o.gamma_theta) * theta, theta) || cmp_le(ph_t - phi, -o.gamma_phi * theta, phi);
-    if (!ok) return false;
+  // ---------------------------------------------------------- filter / acceptor state
+  static constexpr int NLS = 24;  // doubles of LsState when saved
+  struct LsState {
+    double last_mu, wd_th, wd_ph, wd_gbd, wd_alpha, wd_dw, wd_dc, th_max, th_min, dwl, mu_, tau_;
+    int in_wd, wd_short, wd_trial, tiny_last, tiny_flag, in_soft, soft_cnt, last_rej_filter, cnt_filter_rej,
+        n_filter_resets, fallback, acc_count;
+  };
+  LsState ls_;
+  int nfilt_resto_base = 0;
+  int n_resto = 0;
+  bool have_acc = false;
+
+  HTP_HD HTP_FI void ls_reset() {
+    ls_.last_mu = -1.0;
+    ls_.wd_th = ls_.wd_ph = ls_.wd_gbd = ls_.wd_alpha = ls_.wd_dw = ls_.wd_dc = 0.0;
+    ls_.in_wd = ls_.wd_short = ls_.wd_trial = ls_.tiny_last = ls_.tiny_flag = 0;
+    ls_.in_soft = ls_.soft_cnt = ls_.last_rej_filter = ls_.cnt_filter_rej = ls_.n_filter_resets = 0;
+    ls_.fallback = ls_.acc_count = 0;
+  }
+  HTP_HD HTP_FI void ls_save(gd* v) const {
+    if (c.lane == 0) {
+      const double dv[12] = {ls_.last_mu, ls_.wd_th, ls_.wd_ph, ls_.wd_gbd, ls_.wd_alpha, ls_.wd_dw, ls_.wd_dc,
+                             theta_max, theta_min, dw_last, mu, tau};
+      const int iv[12] = {ls_.in_wd, ls_.wd_short, ls_.wd_trial, ls_.tiny_last, ls_.tiny_flag, ls_.in_soft,
+                          ls_.soft_cnt, ls_.last_rej_filter, ls_.cnt_filter_rej, ls_.n_filter_resets, ls_.fallback,
+                          ls_.acc_count};
+      for (int k = 0; k < 12; ++k) { v[k] = dv[k]; v[12 + k] = (double)iv[k]; }
+    }
+    c.sync();
+  }
+  HTP_HD HTP_FI void ls_load(const gd* v) {
+    ls_.last_mu = c.uniform(v[0]); ls_.wd_th = c.uniform(v[1]); ls_.wd_ph = c.uniform(v[2]);
+    ls_.wd_gbd = c.uniform(v[3]); ls_.wd_alpha = c.uniform(v[4]); ls_.wd_dw = c.uniform(v[5]);
+    ls_.wd_dc = c.uniform(v[6]); theta_max = c.uniform(v[7]); theta_min = c.uniform(v[8]);
+    dw_last = c.uniform(v[9]); mu = c.uniform(v[10]); tau = c.uniform(v[11]);
+    int* iv[12] = {&ls_.in_wd, &ls_.wd_short, &ls_.wd_trial, &ls_.tiny_last, &ls_.tiny_flag, &ls_.in_soft,
+                   &ls_.soft_cnt, &ls_.last_rej_filter, &ls_.cnt_filter_rej, &ls_.n_filter_resets, &ls_.fallback,
+                   &ls_.acc_count};
+    for (int k = 0; k < 12; ++k) *iv[k] = (int)c.uniform(v[12 + k]);
+  }
+
+  HTP_HD HTP_FI void filter_add(double theta, double phi) {
+    c.sync();
+    if (c.lane == 0) {
+      if (nfilt < FMAX) { f_th[nfilt] = (1 - o.gamma_theta) * theta; f_ph[nfilt] = phi - o.gamma_phi * theta; }
+      else { for (int k = 1; k < FMAX; ++k) { f_th[k - 1] = f_th[k]; f_ph[k - 1] = f_ph[k]; }
+             f_th[FMAX - 1] = (1 - o.gamma_theta) * theta; f_ph[FMAX - 1] = phi - o.gamma_phi * theta; }
+    }
+    if (nfilt < FMAX) ++nfilt;
+    c.sync();
+  }
+  HTP_HD HTP_FI bool filter_ok(double th_t, double ph_t) const {
     for (int k = 0; k < nfilt; ++k)
       if (!(th_t < f_th[k] || ph_t < f_ph[k])) return false;
     return true;
+  }
+  HTP_HD HTP_FI bool is_ftype(double th, double gbd, double a) const {
+    return gbd < 0 && a * pow(-gbd, o.s_phi) > o.delta * pow(th, o.s_theta);
+  }
+  HTP_HD HTP_FI bool armijo(double ph, double gbd, double a, double ph_t) const {
+    return cmp_le(ph_t - ph, o.eta_phi * a * gbd, ph);
+  }
+  HTP_HD HTP_FI bool acc_to_iterate(double th, double ph, double ph_t, double th_t, bool from_resto) const {
+    if (!from_resto && ph_t > ph) {
+      const double basval = dabs(ph) > 10.0 ? log10(dabs(ph)) : 1.0;
+      if (log10(ph_t - ph) > o.obj_max_inc + basval) return false;
+    }
+    return cmp_le(th_t, (1 - o.gamma_theta) * th, th) || cmp_le(ph_t - ph, -o.gamma_phi * th, ph);
+  }
+  // FilterLSAcceptor::CheckAcceptabilityOfTrialPoint against reference (th, ph, gbd)
+  HTP_HD HTP_FI bool check_trial(double th, double ph, double gbd, double a_test, double th_t, double ph_t) {
+    if (th_t > theta_max || !(ph_t < 1e300)) return false;
+    bool ok;
+    if (a_test > 0 && is_ftype(th, gbd, a_test) && th <= theta_min) ok = armijo(ph, gbd, a_test, ph_t);
+    else ok = acc_to_iterate(th, ph, ph_t, th_t, false);
+    if (!ok) { ls_.last_rej_filter = 0; return false; }
+    if (!filter_ok(th_t, ph_t)) { ls_.last_rej_filter = 1; return false; }
+    return true;
+  }
+  HTP_HD HTP_FI void update_for_next_iteration(double th, double ph, double gbd, double a_test, double ph_t) {
+    if (!(is_ftype(th, gbd, a_test) && armijo(ph, gbd, a_test, ph_t))) filter_add(th, ph);
+    if (o.max_filter_resets > 0) {
+      if (ls_.n_filter_resets < o.max_filter_resets) {
+        if (ls_.last_rej_filter) {
+          if (++ls_.cnt_filter_rej >= o.filter_reset_trigger) {
+            nfilt = 0;
+            ls_.cnt_filter_rej = 0;
+            ++ls_.n_filter_resets;
+          }
+        } else {
+          ls_.cnt_filter_rej = 0;
+        }
+      }
+      ls_.last_rej_filter = 0;
+    }
+  }
+
+  // trial point (xt, st[, Rt]) values: ct, dt, theta, barrier
+  HTP_HD HTP_PHASE void trial_values(const gd* xt, const gd* st, const gd* Rt, double& th_t, double& ph_t) {
+    gd* ct = A(L.ct);
+    gd* dtv = A(L.dt);
+    eval_cons_mode(xt, Rt, ct, dtv);
+    th_t = theta_of(ct, dtv, st);
+    ph_t = barrier(xt, st, Rt, mu, rs);
+  }
+  HTP_HD HTP_FI void set_trial(double alpha, const gd* dx, const gd* ds, const gd* dR) {
+    const gd* x = A(L.x); const gd* s = A(L.s);
+    gd* xt = A(L.xt); gd* st = A(L.st);
+    {
+      double a_[SW_U], b_[SW_U];
+      sweep(D.n, [&](int q, int k) { a_[k] = x[q]; b_[k] = dx[q]; }, [&](int q, int k) { xt[q] = a_[k] + alpha * b_[k]; });
+      sweep(D.md, [&](int r, int k) { a_[k] = s[r]; b_[k] = ds[r]; }, [&](int r, int k) { st[r] = a_[k] + alpha * b_[k]; });
+    }
+    if (rs) {
+      const gd* R = A(L.R);
+      gd* Rt = A(L.Rt);
+      for (int j = c.lane; j < nR; j += c.width) Rt[j] = R[j] + alpha * dR[j];
+    }
+    c.sync();
+  }
+
+  HTP_HD HTP_FI void copy_arr(gd* dst, const gd* src, int n) {
+    double a_[SW_U];
+    sweep(n, [&](int q, int k) { a_[k] = src[q]; }, [&](int q, int k) { dst[q] = a_[k]; });
+    c.sync();
   }
 
   HTP_HD HTP_FI void run(Result& res) {
@@ -2853,6 +3200,11 @@ struct ObcaSolver {
     for (int k = 0; k < 8; ++k) cyc[k] = 0;
     dw_last = 0.0;
     nfilt = 0;
+    rs = false;
+    nR = 2 * D.mc + 2 * D.md;
+    n_resto = 0;
+    have_acc = false;
+    ls_reset();
     set_bounds_and_x0();
     HTP_TRACE("[trace] bounds\n");
     compute_scaling();
@@ -2879,53 +3231,10 @@ struct ObcaSolver {
         vL[r] = o.bound_mult_init_val;
         vU[r] = finite_(dU[r]) ? o.bound_mult_init_val : 0.0;
       }
-      gd* yc = A(L.yc); gd* yd = A(L.yd);
-      HTP_UNROLL
-      for (int r = c.lane; r < D.mc; r += c.width) yc[r] = 0.0;
-      HTP_UNROLL
-      for (int r = c.lane; r < D.md; r += c.width) yd[r] = 0.0;
       c.sync();
     }
     eval_grad_f(x, A(L.gf), sf);
-    // least-squares multipliers
-    {
-      int neg, zero;
-      factorize(true, 0.0, 0.0, neg, zero);
-      ++n_factor;
-      HTP_TRACE("[trace] LS factor neg=%d zero=%d\n", neg, zero);
-#ifdef HTP_HOST_DEBUG
-      printf("[dbg] LS factor neg=%d need=%d zero=%d\n", neg, D.mc + D.md, zero);
-#endif
-      if (neg == D.mc + D.md && zero == 0) {
-        gd* bx = A(L.rx); gd* bs = A(L.rs); gd* bc = A(L.rc); gd* bd = A(L.rd);
-        const gd* gf = A(L.gf);
-        const gd* zL = A(L.zL); const gd* zU = A(L.zU); const gd* vL = A(L.vL); const gd* vU = A(L.vU);
-        HTP_UNROLL
-        for (int q = c.lane; q < D.n; q += c.width) bx[q] = -(gf[q] - zL[q] + zU[q]);
-        HTP_UNROLL
-        for (int r = c.lane; r < D.md; r += c.width) { bs[r] = -(-vL[r] + vU[r]); bd[r] = 0.0; }
-        HTP_UNROLL
-        for (int r = c.lane; r < D.mc; r += c.width) bc[r] = 0.0;
-        c.sync();
-        kkt_solve(true, 0.0, 0.0, bx, bs, bc, bd, A(L.dx), A(L.ds), A(L.dyc), A(L.dyd));
-        HTP_TRACE("[trace] LS solve\n");
-        const gd* a1 = A(L.dyc); const gd* a2 = A(L.dyd);
-        double mx = 0.0;
-        HTP_UNROLL
-        for (int r = c.lane; r < D.mc; r += c.width) mx = dmax(mx, dabs(a1[r]));
-        HTP_UNROLL
-        for (int r = c.lane; r < D.md; r += c.width) mx = dmax(mx, dabs(a2[r]));
-        mx = c.maxv(mx);
-        if (mx <= o.constr_mult_init_max) {
-          gd* yc = A(L.yc); gd* yd = A(L.yd);
-          HTP_UNROLL
-          for (int r = c.lane; r < D.mc; r += c.width) yc[r] = a1[r];
-          HTP_UNROLL
-          for (int r = c.lane; r < D.md; r += c.width) yd[r] = a2[r];
-        }
-        c.sync();
-      }
-    }
+    ls_multipliers();
     mu = o.mu_init;
     tau = dmax(o.tau_min, 1.0 - mu);
     {
@@ -2935,235 +3244,761 @@ struct ObcaSolver {
     }
   }
 
+  // least-squares constraint multipliers [I 0 Jc' Jd'; 0 I 0 -I; Jc 0 0 0; Jd -I 0 0] (current mode);
+  // y = 0 unless the inertia is right and |y|_inf <= constr_mult_init_max
+  HTP_HD HTP_FI void ls_multipliers() {
+    gd* yc = A(L.yc); gd* yd = A(L.yd);
+    HTP_UNROLL
+    for (int r = c.lane; r < D.mc; r += c.width) yc[r] = 0.0;
+    HTP_UNROLL
+    for (int r = c.lane; r < D.md; r += c.width) yd[r] = 0.0;
+    c.sync();
+    int neg, zero;
+    factorize(true, 0.0, 0.0, neg, zero);
+    ++n_factor;
+    HTP_TRACE("[trace] LS factor neg=%d zero=%d\n", neg, zero);
+    if (!(neg == D.mc + D.md && zero == 0)) return;
+    gd* bx = A(L.rx); gd* bs = A(L.rs); gd* bc = A(L.rc); gd* bd = A(L.rd);
+    const gd* gf = A(L.gf);
+    const gd* zL = A(L.zL); const gd* zU = A(L.zU); const gd* vL = A(L.vL); const gd* vU = A(L.vU);
+    HTP_UNROLL
+    for (int q = c.lane; q < D.n; q += c.width) bx[q] = -(gf[q] - zL[q] + zU[q]);
+    HTP_UNROLL
+    for (int r = c.lane; r < D.md; r += c.width) { bs[r] = -(-vL[r] + vU[r]); bd[r] = 0.0; }
+    HTP_UNROLL
+    for (int r = c.lane; r < D.mc; r += c.width) bc[r] = 0.0;
+    gd* bR = A(L.rRx);
+    if (rs) {
+      const gd* zR = A(L.zR);
+      for (int j = c.lane; j < nR; j += c.width) bR[j] = -(o.resto_penalty_parameter - zR[j]);
+    }
+    c.sync();
+    kkt_solve(true, 0.0, 0.0, bx, bs, bc, bd, A(L.dx), A(L.ds), A(L.dyc), A(L.dyd), bR, A(L.dR));
+    HTP_TRACE("[trace] LS solve\n");
+    const gd* a1 = A(L.dyc); const gd* a2 = A(L.dyd);
+    double mx = 0.0;
+    HTP_UNROLL
+    for (int r = c.lane; r < D.mc; r += c.width) mx = dmax(mx, dabs(a1[r]));
+    HTP_UNROLL
+    for (int r = c.lane; r < D.md; r += c.width) mx = dmax(mx, dabs(a2[r]));
+    mx = c.maxv(mx);
+    if (mx <= o.constr_mult_init_max) {
+      HTP_UNROLL
+      for (int r = c.lane; r < D.mc; r += c.width) yc[r] = a1[r];
+      HTP_UNROLL
+      for (int r = c.lane; r < D.md; r += c.width) yd[r] = a2[r];
+    }
+    c.sync();
+  }
+
+  // Newton right-hand side at the current point: rx (into xt), rs, rc, rd[, rRx] ; gbx (sx), gbs (ss)
+  // returns the directional-derivative factors via gBD once the step exists (newton_gbd)
+  HTP_HD HTP_FI void build_newton_rhs(const gd* gl) {
+    gd* gbx = A(L.sx); gd* gbs = A(L.ss);
+    grad_barrier(mu, gbx, gbs);
+    gd* rx = A(L.xt);
+    gd* rs_ = A(L.rs); gd* rc = A(L.rc); gd* rd = A(L.rd);
+    const gd* gf = A(L.gf); const gd* yd = A(L.yd); const gd* cc = A(L.c); const gd* dd = A(L.d);
+    const gd* s = A(L.s);
+    {
+      double a_[SW_U], b_[SW_U], g_[SW_U];
+      sweep(D.n, [&](int q, int k) { a_[k] = gl[q]; b_[k] = gf[q]; g_[k] = gbx[q]; },
+            [&](int q, int k) { rx[q] = -(a_[k] - b_[k] + g_[k]); });
+    }
+    {
+      double a_[SW_U], b_[SW_U], d_[SW_U], s_[SW_U];
+      sweep(D.md, [&](int r, int k) { a_[k] = gbs[r]; b_[k] = yd[r]; d_[k] = dd[r]; s_[k] = s[r]; },
+            [&](int r, int k) { rs_[r] = -(a_[k] - b_[k]); rd[r] = -(d_[k] - s_[k]); });
+    }
+    {
+      double a_[SW_U];
+      sweep(D.mc, [&](int r, int k) { a_[k] = cc[r]; }, [&](int r, int k) { rc[r] = -a_[k]; });
+    }
+    if (rs) {
+      const gd* R = A(L.R); const gd* yc = A(L.yc);
+      gd* rR = A(L.rRx);
+      for (int j = c.lane; j < nR; j += c.width) rR[j] = -(np_grad_barrier(j, R, mu) + np_jty(j, yc, A(L.yd)));
+    }
+    c.sync();
+  }
+  // gradient of the barrier function along (dx, ds[, dR]); gbx, gbs must be current (sx, ss)
+  HTP_HD HTP_FI double newton_gbd(const gd* dx, const gd* ds, const gd* dR) {
+    const gd* gbx = A(L.sx); const gd* gbs = A(L.ss);
+    double g = 0.0;
+    {
+      double a_[SW_U], b_[SW_U];
+      sweep(D.n, [&](int q, int k) { a_[k] = gbx[q]; b_[k] = dx[q]; }, [&](int, int k) { g += a_[k] * b_[k]; });
+      sweep(D.md, [&](int r, int k) { a_[k] = gbs[r]; b_[k] = ds[r]; }, [&](int, int k) { g += a_[k] * b_[k]; });
+    }
+    if (rs) {
+      const gd* R = A(L.R);
+      for (int j = c.lane; j < nR; j += c.width) g += np_grad_barrier(j, R, mu) * dR[j];
+    }
+    return c.sum(g);
+  }
+
+  // accept the trial step alpha along (dx, ds, dyc, dyd[, dR]): primal from x + a dx (bitwise the trial
+  // point), dual step with a_dual, kappa_Sigma safeguard; constraint values from the trial (ct, dt)
+  HTP_HD HTP_FI void accept_step(double a_primal, double a_dual, const gd* dx, const gd* ds, const gd* dyc,
+                                 const gd* dyd, const gd* dR) {
+    gd* x = A(L.x); gd* s = A(L.s);
+    gd* zL = A(L.zL); gd* zU = A(L.zU); gd* vL = A(L.vL); gd* vU = A(L.vU);
+    gd* yc = A(L.yc); gd* yd = A(L.yd);
+    const gd* dzL = A(L.dzL); const gd* dzU = A(L.dzU);
+    const gd* dvL = A(L.dvL); const gd* dvU = A(L.dvU);
+    gd* xL = A(L.xL); gd* xU = A(L.xU);
+    gd* dL = A(L.dL); gd* dU = A(L.dU);
+    const double ks = o.kappa_sigma;
+    {
+      double x_[SW_U], d_[SW_U], xl_[SW_U], xu_[SW_U], zl_[SW_U], zu_[SW_U], dzl_[SW_U], dzu_[SW_U];
+      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; d_[k] = dx[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; zl_[k] = zL[q];
+                                      zu_[k] = zU[q]; dzl_[k] = dzL[q]; dzu_[k] = dzU[q]; },
+            [&](int q, int k) {
+              const double xn = x_[k] + a_primal * d_[k];
+              x[q] = xn;
+              if (finite_(xl_[k])) {
+                const double v0 = xn - xl_[k], v = safe_slack(v0, zl_[k], xl_[k], mu);
+                if (v != v0) xL[q] = xn - v;
+                const double z = zl_[k] + a_dual * dzl_[k];
+                zL[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v));
+              }
+              if (finite_(xu_[k])) {
+                const double v0 = xu_[k] - xn, v = safe_slack(v0, zu_[k], xu_[k], mu);
+                if (v != v0) xU[q] = xn + v;
+                const double z = zu_[k] + a_dual * dzu_[k];
+                zU[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v));
+              }
+            });
+    }
+    {
+      double s_[SW_U], d_[SW_U], y_[SW_U], dy_[SW_U], vl_[SW_U], dvl_[SW_U], dl_[SW_U], vu_[SW_U], dvu_[SW_U], du_[SW_U];
+      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; d_[k] = ds[r]; y_[k] = yd[r]; dy_[k] = dyd[r]; vl_[k] = vL[r];
+                                       dvl_[k] = dvL[r]; dl_[k] = dL[r]; vu_[k] = vU[r]; dvu_[k] = dvU[r]; du_[k] = dU[r]; },
+            [&](int r, int k) {
+              const double sn = s_[k] + a_primal * d_[k];
+              s[r] = sn;
+              yd[r] = y_[k] + a_primal * dy_[k];
+              {
+                const double v0 = sn - dl_[k], v = safe_slack(v0, vl_[k], dl_[k], mu);
+                if (v != v0) dL[r] = sn - v;
+                const double z = vl_[k] + a_dual * dvl_[k];
+                vL[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v));
+              }
+              if (finite_(du_[k])) {
+                const double v0 = du_[k] - sn, v = safe_slack(v0, vu_[k], du_[k], mu);
+                if (v != v0) dU[r] = sn + v;
+                const double z = vu_[k] + a_dual * dvu_[k];
+                vU[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v));
+              }
+            });
+    }
+    {
+      double y_[SW_U], dy_[SW_U];
+      sweep(D.mc, [&](int r, int k) { y_[k] = yc[r]; dy_[k] = dyc[r]; },
+            [&](int r, int k) { yc[r] = y_[k] + a_primal * dy_[k]; });
+    }
+    if (rs) {
+      gd* R = A(L.R); gd* zR = A(L.zR);
+      const gd* dzR = A(L.dzR);
+      for (int j = c.lane; j < nR; j += c.width) {
+        const double rn = R[j] + a_primal * dR[j];
+        R[j] = rn;
+        const double z = zR[j] + a_dual * dzR[j];
+        zR[j] = dmax(dmin(z, ks * mu / rn), mu / (ks * rn));
+      }
+    }
+    c.sync();
+    copy_arr(A(L.c), A(L.ct), D.mc);
+    copy_arr(A(L.d), A(L.dt), D.md);
+  }
+
+  // IpBacktrackingLineSearch::DetectTinyStep (x includes R in the restoration phase)
+  HTP_HD HTP_FI bool detect_tiny_step(const gd* dx, const gd* ds, const gd* dyc, const gd* dyd, const gd* dR) {
+    if (o.tiny_step_tol == 0.0) return false;
+    const gd* x = A(L.x); const gd* s = A(L.s); const gd* cc = A(L.c); const gd* dd = A(L.d);
+    double mx = 0.0, ms = 0.0, my = 0.0, pv = 0.0;
+    for (int q = c.lane; q < D.n; q += c.width) mx = dmax(mx, dabs(dx[q]) / (1.0 + dabs(x[q])));
+    if (rs) {
+      const gd* R = A(L.R);
+      for (int j = c.lane; j < nR; j += c.width) mx = dmax(mx, dabs(dR[j]) / (1.0 + dabs(R[j])));
+    }
+    for (int r = c.lane; r < D.md; r += c.width) {
+      ms = dmax(ms, dabs(ds[r]) / (1.0 + dabs(s[r])));
+      my = dmax(my, dabs(dyd[r]));
+      pv = dmax(pv, dabs(dd[r] - s[r]));
+    }
+    for (int r = c.lane; r < D.mc; r += c.width) {
+      my = dmax(my, dabs(dyc[r]));
+      pv = dmax(pv, dabs(cc[r]));
+    }
+    mx = c.maxv(mx); ms = c.maxv(ms); my = c.maxv(my); pv = c.maxv(pv);
+    if (mx > o.tiny_step_tol || ms > o.tiny_step_tol) return false;
+    if (my >= o.tiny_step_y_tol) return false;
+    if (pv > 1e-4) return false;
+    return true;
+  }
+
+  // ---------------------------------------------------------- watchdog
+  // stores the current point, its constraint values, the step and the reference values
+  __attribute__((noinline)) HTP_HD void start_watchdog(double th, double ph, double gbd, double dw, double dc) {
+    ls_.in_wd = 1;
+    ls_.wd_th = th; ls_.wd_ph = ph; ls_.wd_gbd = gbd; ls_.wd_dw = dw; ls_.wd_dc = dc;
+    ls_.wd_trial = 0;
+    ls_.wd_alpha = frac_primal(A(L.dx), A(L.ds), A(L.dR));
+    copy_arr(A(L.wx), A(L.x), D.n); copy_arr(A(L.ws), A(L.s), D.md);
+    copy_arr(A(L.wyc), A(L.yc), D.mc); copy_arr(A(L.wyd), A(L.yd), D.md);
+    copy_arr(A(L.wzL), A(L.zL), D.n); copy_arr(A(L.wzU), A(L.zU), D.n);
+    copy_arr(A(L.wvL), A(L.vL), D.md); copy_arr(A(L.wvU), A(L.vU), D.md);
+    copy_arr(A(L.wc), A(L.c), D.mc); copy_arr(A(L.wd), A(L.d), D.md);
+    copy_arr(A(L.wdx), A(L.dx), D.n); copy_arr(A(L.wds), A(L.ds), D.md);
+    copy_arr(A(L.wdyc), A(L.dyc), D.mc); copy_arr(A(L.wdyd), A(L.dyd), D.md);
+    if (rs) { copy_arr(A(L.wR), A(L.R), nR); copy_arr(A(L.wzR), A(L.zR), nR); copy_arr(A(L.wdR), A(L.dR), nR); }
+  }
+  // back to the stored point and step; its gradients, Newton rhs and the stored matrix (for SOC)
+  __attribute__((noinline)) HTP_HD void stop_watchdog() {
+    ls_.in_wd = 0;
+    copy_arr(A(L.x), A(L.wx), D.n); copy_arr(A(L.s), A(L.ws), D.md);
+    copy_arr(A(L.yc), A(L.wyc), D.mc); copy_arr(A(L.yd), A(L.wyd), D.md);
+    copy_arr(A(L.zL), A(L.wzL), D.n); copy_arr(A(L.zU), A(L.wzU), D.n);
+    copy_arr(A(L.vL), A(L.wvL), D.md); copy_arr(A(L.vU), A(L.wvU), D.md);
+    copy_arr(A(L.c), A(L.wc), D.mc); copy_arr(A(L.d), A(L.wd), D.md);
+    copy_arr(A(L.dx), A(L.wdx), D.n); copy_arr(A(L.ds), A(L.wds), D.md);
+    copy_arr(A(L.dyc), A(L.wdyc), D.mc); copy_arr(A(L.dyd), A(L.wdyd), D.md);
+    if (rs) { copy_arr(A(L.R), A(L.wR), nR); copy_arr(A(L.zR), A(L.wzR), nR); copy_arr(A(L.dR), A(L.wdR), nR); }
+    eval_grad_mode(A(L.x));
+    gd* gl = A(L.rx);
+    grad_lag_into(gl);
+    build_newton_rhs(gl);
+    int neg, zero;
+    factorize(false, ls_.wd_dw, ls_.wd_dc, neg, zero);
+    ++n_factor;
+    ls_.wd_short = 0;
+  }
+
+  // ---------------------------------------------------------- line search
+  // DoBacktrackingLineSearch with second-order corrections.  On return the trial point (xt, st[, Rt],
+  // ct, dt) holds the last tested point; the step arrays hold the direction actually taken.
+  HTP_HD HTP_PHASE bool backtrack(double th, double ph, double gbd, bool skip_first, int& n_steps,
+                                  double& a_primal, double& a_test, double& ph_acc, double& th_acc,
+                                  double dw, double dc) {
+    gd* x = A(L.x); gd* s = A(L.s);
+    gd* dx = A(L.dx); gd* ds = A(L.ds); gd* dyc = A(L.dyc); gd* dyd = A(L.dyd); gd* dR = A(L.dR);
+    const gd* cc = A(L.c); const gd* dd = A(L.d);
+    const double alpha_max = frac_primal(dx, ds, dR);
+    double alpha_min;
+    if (ls_.in_wd) {
+      alpha_min = alpha_max;
+    } else {
+      alpha_min = o.gamma_theta;
+      if (gbd < 0) {
+        alpha_min = dmin(o.gamma_theta, o.gamma_phi * th / (-gbd));
+        if (th <= theta_min) alpha_min = dmin(alpha_min, o.delta * pow(th, o.s_theta) / pow(-gbd, o.s_phi));
+      }
+      alpha_min *= o.alpha_min_frac;
+    }
+    double alpha = alpha_max;
+    if (skip_first) alpha *= 0.5;
+    bool accept = false;
+    const double theta_curr = th;  // the reference point is the current point here
+    double th_t = 0.0, ph_t = 0.0;
+    gd* xt = A(L.xt); gd* st = A(L.st); gd* Rt = A(L.Rt);
+    while (alpha > alpha_min || n_steps == 0) {
+      set_trial(alpha, dx, ds, dR);
+      trial_values(xt, st, Rt, th_t, ph_t);
+      a_test = ls_.in_wd ? ls_.wd_alpha : alpha;
+      if (check_trial(th, ph, gbd, a_test, th_t, ph_t)) { accept = true; break; }
+      HTP_TRACE("[trace]   ls alpha=%.17g th_t=%.17g ph_t=%.17g (theta=%.17g phi=%.17g gBD=%.17g amax=%.17g)\n", alpha, th_t, ph_t, th, ph, gbd, alpha_max);
+      if (ls_.in_wd) break;
+      if (alpha == alpha_max && theta_curr <= th_t && o.max_soc > 0) {
+        // second-order corrections (IPOPT TrySecondOrderCorrection); rhs x part is rxk (sx)
+        gd* csoc = A(L.csoc); gd* dsoc = A(L.dsoc);
+        const gd* ct = A(L.ct); const gd* dtv = A(L.dt);
+        HTP_UNROLL
+        for (int r = c.lane; r < D.mc; r += c.width) csoc[r] = alpha * cc[r] + ct[r];
+        HTP_UNROLL
+        for (int r = c.lane; r < D.md; r += c.width) dsoc[r] = alpha * (dd[r] - s[r]) + (dtv[r] - st[r]);
+        c.sync();
+        double th_old = th;
+        gd* sx = A(L.dzL);  // temporaries (dz arrays are recomputed after acceptance)
+        gd* ss_ = A(L.dvL); gd* syc = A(L.syc); gd* syd = A(L.syd); gd* sR = A(L.dzR);
+        gd* nrc = A(L.ct); gd* nrd = A(L.dt);
+        const gd* rxk = A(L.sx);
+        bool soc_ok = false;
+        for (int k = 0; k < o.max_soc; ++k) {
+          HTP_UNROLL
+          for (int r = c.lane; r < D.mc; r += c.width) nrc[r] = -csoc[r];
+          HTP_UNROLL
+          for (int r = c.lane; r < D.md; r += c.width) nrd[r] = -dsoc[r];
+          c.sync();
+          kkt_solve(false, dw, dc, rxk, A(L.rs), nrc, nrd, sx, ss_, syc, syd, A(L.rRx), sR);
+          const double a_soc = frac_primal(sx, ss_, sR);
+          set_trial(a_soc, sx, ss_, sR);
+          double th_soc, ph_soc;
+          trial_values(xt, st, Rt, th_soc, ph_soc);
+          if (check_trial(th, ph, gbd, a_test, th_soc, ph_soc)) {
+            soc_ok = true; alpha = a_soc; th_t = th_soc; ph_t = ph_soc;
+            copy_arr(dx, sx, D.n); copy_arr(ds, ss_, D.md); copy_arr(dyc, syc, D.mc); copy_arr(dyd, syd, D.md);
+            if (rs) copy_arr(dR, sR, nR);
+            break;
+          }
+          if (th_soc > o.kappa_soc * th_old) break;
+          th_old = th_soc;
+          const gd* ct2 = A(L.ct); const gd* dt2 = A(L.dt);
+          HTP_UNROLL
+          for (int r = c.lane; r < D.mc; r += c.width) csoc[r] = a_soc * csoc[r] + ct2[r];
+          HTP_UNROLL
+          for (int r = c.lane; r < D.md; r += c.width) dsoc[r] = a_soc * dsoc[r] + (dt2[r] - st[r]);
+          c.sync();
+        }
+        if (soc_ok) { accept = true; break; }
+      }
+      alpha *= 0.5;
+      ++n_steps;
+    }
+    a_primal = alpha;
+    ph_acc = ph_t;
+    th_acc = th_t;
+    if (accept) update_for_next_iteration(th, ph, gbd, a_test, ph_t);
+    (void)x;
+    return accept;
+  }
+
+  // TrySoftRestoStep: the primal-dual step with alpha = min(primal, dual fraction to the boundary).
+  // Returns 0 (rejected: nothing changed), 1 (accepted: primal-dual error reduced), 2 (accepted and
+  // acceptable to the original filter criteria).  On acceptance the new iterate is in place.
+  __attribute__((noinline)) HTP_HD int try_soft_resto_step(double th, double ph, double gbd, const gd* gl) {
+    const gd* dx = A(L.dx); const gd* ds = A(L.ds); const gd* dyc = A(L.dyc); const gd* dyd = A(L.dyd);
+    const gd* dR = A(L.dR);
+    const double ap = frac_primal(dx, ds, dR);
+    const double ad = dual_steps(dx, ds, dR);
+    const double a = dmin(ap, ad);
+    set_trial(a, dx, ds, dR);
+    gd* xt = A(L.xt); gd* st = A(L.st); gd* Rt = A(L.Rt);
+    double th_t, ph_t;
+    trial_values(xt, st, Rt, th_t, ph_t);
+    // trial multipliers (the watchdog arrays are free whenever this runs)
+    gd* tyc = A(L.wyc); gd* tyd = A(L.wyd); gd* tzL = A(L.wzL); gd* tzU = A(L.wzU);
+    gd* tvL = A(L.wvL); gd* tvU = A(L.wvU); gd* tzR = A(L.wzR);
+    {
+      const gd* xL = A(L.xL); const gd* xU = A(L.xU); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
+      const gd* yc = A(L.yc); const gd* yd = A(L.yd); const gd* zL = A(L.zL); const gd* zU = A(L.zU);
+      const gd* vL = A(L.vL); const gd* vU = A(L.vU);
+      const gd* dzL = A(L.dzL); const gd* dzU = A(L.dzU); const gd* dvL = A(L.dvL); const gd* dvU = A(L.dvU);
+      const double ks = o.kappa_sigma;
+      for (int q = c.lane; q < D.n; q += c.width) {
+        tzL[q] = zL[q]; tzU[q] = zU[q];
+        if (finite_(xL[q])) { const double z = zL[q] + a * dzL[q], v = safe_slack(xt[q] - xL[q], zL[q], xL[q], mu); tzL[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+        if (finite_(xU[q])) { const double z = zU[q] + a * dzU[q], v = safe_slack(xU[q] - xt[q], zU[q], xU[q], mu); tzU[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+      }
+      for (int r = c.lane; r < D.md; r += c.width) {
+        tyd[r] = yd[r] + a * dyd[r];
+        { const double z = vL[r] + a * dvL[r], v = safe_slack(st[r] - dL[r], vL[r], dL[r], mu); tvL[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+        tvU[r] = vU[r];
+        if (finite_(dU[r])) { const double z = vU[r] + a * dvU[r], v = safe_slack(dU[r] - st[r], vU[r], dU[r], mu); tvU[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
+      }
+      for (int r = c.lane; r < D.mc; r += c.width) tyc[r] = yc[r] + a * dyc[r];
+      if (rs) {
+        const gd* zR = A(L.zR); const gd* dzR = A(L.dzR);
+        for (int j = c.lane; j < nR; j += c.width) {
+          const double z = zR[j] + a * dzR[j], v = Rt[j];
+          tzR[j] = dmax(dmin(z, ks * mu / v), mu / (ks * v));
+        }
+      }
+      c.sync();
+    }
+    const int sat = check_trial(th, ph, gbd, 0.0, th_t, ph_t) ? 1 : 0;
+    if (!sat) {
+      const double e_cur = pd_error(gl, A(L.x), A(L.s), A(L.yc), A(L.yd), A(L.zL), A(L.zU), A(L.vL), A(L.vU),
+                                    A(L.R), A(L.zR), A(L.c), A(L.d), mu);
+      gd* gft = A(L.dzL); gd* glt = A(L.dzU);
+      if (rs) eval_grad_f_rs(xt, gft);
+      else eval_grad_f(xt, gft, sf);
+      grad_lag_at(xt, tyc, tyd, gft, glt);
+      const double e_tr = pd_error(glt, xt, st, tyc, tyd, tzL, tzU, tvL, tvU, Rt, tzR, A(L.ct), A(L.dt), mu, true);
+      if (!(e_tr <= o.soft_resto_pderror_reduction_factor * e_cur)) return 0;
+    }
+    {  // AdjustVariableBounds for slacks the safe-slack rule corrected (current multipliers)
+      gd* xL = A(L.xL); gd* xU = A(L.xU); gd* dL = A(L.dL); gd* dU = A(L.dU);
+      const gd* zL = A(L.zL); const gd* zU = A(L.zU); const gd* vL = A(L.vL); const gd* vU = A(L.vU);
+      for (int q = c.lane; q < D.n; q += c.width) {
+        if (finite_(xL[q])) { const double v0 = xt[q] - xL[q], v = safe_slack(v0, zL[q], xL[q], mu); if (v != v0) xL[q] = xt[q] - v; }
+        if (finite_(xU[q])) { const double v0 = xU[q] - xt[q], v = safe_slack(v0, zU[q], xU[q], mu); if (v != v0) xU[q] = xt[q] + v; }
+      }
+      for (int r = c.lane; r < D.md; r += c.width) {
+        { const double v0 = st[r] - dL[r], v = safe_slack(v0, vL[r], dL[r], mu); if (v != v0) dL[r] = st[r] - v; }
+        if (finite_(dU[r])) { const double v0 = dU[r] - st[r], v = safe_slack(v0, vU[r], dU[r], mu); if (v != v0) dU[r] = st[r] + v; }
+      }
+      c.sync();
+    }
+    copy_arr(A(L.x), xt, D.n); copy_arr(A(L.s), st, D.md);
+    copy_arr(A(L.yc), tyc, D.mc); copy_arr(A(L.yd), tyd, D.md);
+    copy_arr(A(L.zL), tzL, D.n); copy_arr(A(L.zU), tzU, D.n); copy_arr(A(L.vL), tvL, D.md); copy_arr(A(L.vU), tvU, D.md);
+    if (rs) { copy_arr(A(L.R), Rt, nR); copy_arr(A(L.zR), tzR, nR); }
+    copy_arr(A(L.c), A(L.ct), D.mc); copy_arr(A(L.d), A(L.dt), D.md);
+    eval_grad_mode(A(L.x));
+    return sat ? 2 : 1;
+  }
+
+  // n/p in closed form for the constraint residuals (cv) of row j (IpRestoIterateInitializer::solve_quadratic)
+  HTP_HD HTP_FI static void np_closed_form(double cv, double mu_, double rho, double& nv, double& pv) {
+    const double a = mu_ / (2.0 * rho) - 0.5 * cv;
+    nv = a + sqrt(a * a + cv * mu_ / (2.0 * rho));
+    pv = cv + nv;
+  }
+  // R (and zR = mu / R) from original residuals c (cres, mc) and d - s (dres, md)
+  HTP_HD HTP_FI void np_init(const gd* cres, const gd* dv, const gd* s, double mu_) {
+    gd* R = A(L.R); gd* zR = A(L.zR);
+    const int mc = D.mc, md = D.md;
+    const double rho = o.resto_penalty_parameter;
+    for (int r = c.lane; r < mc; r += c.width) {
+      double nv, pv;
+      np_closed_form(cres[r], mu_, rho, nv, pv);
+      R[r] = nv; R[mc + r] = pv; zR[r] = mu_ / nv; zR[mc + r] = mu_ / pv;
+    }
+    for (int r = c.lane; r < md; r += c.width) {
+      double nv, pv;
+      np_closed_form(dv[r] - s[r], mu_, rho, nv, pv);
+      R[2 * mc + r] = nv; R[2 * mc + md + r] = pv; zR[2 * mc + r] = mu_ / nv; zR[2 * mc + md + r] = mu_ / pv;
+    }
+    c.sync();
+  }
+
+  // MinC_1NrmRestorationPhase: save the original iterate and state, set up the restoration problem
+  // (RestoIterateInitializer) at the current point
+  __attribute__((noinline)) HTP_HD void enter_resto(double th, double ph, double gbd) {
+    gd* osv = A(L.osv);
+    ls_save(osv);
+    if (c.lane == 0) { osv[24] = th; osv[25] = ph; osv[26] = gbd; osv[27] = (double)nfilt; }
+    {
+      gd* of = A(L.ofilt);
+      if (c.lane == 0)
+        for (int k = 0; k < nfilt; ++k) { of[k] = f_th[k]; of[FMAX + k] = f_ph[k]; }
+      c.sync();
+    }
+    gd* x = A(L.x); gd* s = A(L.s); gd* cc = A(L.c); gd* dd = A(L.d);
+    copy_arr(A(L.ox), x, D.n); copy_arr(A(L.os), s, D.md);
+    copy_arr(A(L.oyc), A(L.yc), D.mc); copy_arr(A(L.oyd), A(L.yd), D.md);
+    copy_arr(A(L.ozL), A(L.zL), D.n); copy_arr(A(L.ozU), A(L.zU), D.n);
+    copy_arr(A(L.ovL), A(L.vL), D.md); copy_arr(A(L.ovU), A(L.vU), D.md);
+    double m = mu;
+    for (int r = c.lane; r < D.mc; r += c.width) m = dmax(m, dabs(cc[r]));
+    for (int r = c.lane; r < D.md; r += c.width) m = dmax(m, dabs(dd[r] - s[r]));
+    const double mu_r = c.maxv(m);
+    const double rho = o.resto_penalty_parameter;
+    {
+      gd* xR = A(L.xR); gd* dr = A(L.dr);
+      for (int q = c.lane; q < D.n; q += c.width) { xR[q] = x[q]; dr[q] = 1.0 / dmax(1.0, dabs(x[q])); }
+    }
+    np_init(cc, dd, s, mu_r);
+    {
+      gd* zL = A(L.zL); gd* zU = A(L.zU); gd* vL = A(L.vL); gd* vU = A(L.vU);
+      for (int q = c.lane; q < D.n; q += c.width) { zL[q] = dmin(rho, zL[q]); zU[q] = dmin(rho, zU[q]); }
+      for (int r = c.lane; r < D.md; r += c.width) { vL[r] = dmin(rho, vL[r]); vU[r] = dmin(rho, vU[r]); }
+      c.sync();
+    }
+    rs = true;
+    mu = mu_r;
+    tau = dmax(o.tau_min, 1.0 - mu);
+    eta = o.resto_proximity_weight * sqrt(mu);
+    {  // restoration constraint values c + n - p, d + n_d - p_d
+      const gd* R = A(L.R);
+      const int mc = D.mc, md = D.md;
+      for (int r = c.lane; r < mc; r += c.width) cc[r] += R[r] - R[mc + r];
+      for (int r = c.lane; r < md; r += c.width) dd[r] += R[2 * mc + r] - R[2 * mc + md + r];
+      c.sync();
+    }
+    eval_grad_f_rs(x, A(L.gf));
+    ls_multipliers();
+    nfilt = 0;
+    dw_last = 0.0;
+    ls_reset();
+    const double th0 = theta_of(cc, dd, s);
+    theta_max = 1e4 * dmax(1.0, th0);
+    theta_min = 1e-4 * dmax(1.0, th0);
+    ++n_resto;
+  }
+
+  // RestoConvergenceCheck: original theta reduced by required_infeasibility_reduction and the point
+  // acceptable to the original filter and to the original iterate
+  HTP_HD HTP_FI bool resto_converged() {
+    const gd* osv = A(L.osv);
+    const gd* s = A(L.s);
+    const double th_R = c.uniform(osv[24]), ph_R = c.uniform(osv[25]), mu_o = c.uniform(osv[10]);
+    const int nf = (int)c.uniform(osv[27]);
+    const double th_o = orig_theta_rs(A(L.c), A(L.d), s, A(L.R));
+    if (th_o > o.required_infeasibility_reduction * th_R) return false;
+    const double ph_o = barrier(A(L.x), s, A(L.R), mu_o, false);
+    const gd* of = A(L.ofilt);
+    for (int k = 0; k < nf; ++k)
+      if (!(th_o < of[k] || ph_o < of[FMAX + k])) return false;
+    return acc_to_iterate(th_R, ph_R, ph_o, th_o, true);
+  }
+
+  // back to the original problem with x, s of the restoration phase: bound multipliers take one
+  // complementarity Newton step for the whole primal change (all reset to 1 if > threshold), y = 0
+  __attribute__((noinline)) HTP_HD void leave_resto() {
+    rs = false;
+    const gd* osv = A(L.osv);
+    ls_load(osv);
+    nfilt = (int)c.uniform(osv[27]);
+    {
+      const gd* of = A(L.ofilt);
+      if (c.lane == 0)
+        for (int k = 0; k < nfilt; ++k) { f_th[k] = of[k]; f_ph[k] = of[FMAX + k]; }
+      c.sync();
+    }
+    gd* x = A(L.x); gd* s = A(L.s);
+    eval_cons(x, A(L.c), A(L.d));
+    const gd* xL = A(L.xL); const gd* xU = A(L.xU); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
+    const gd* ox = A(L.ox); const gd* os = A(L.os);
+    const gd* ozL = A(L.ozL); const gd* ozU = A(L.ozU); const gd* ovL = A(L.ovL); const gd* ovU = A(L.ovU);
+    gd* dzL = A(L.dzL); gd* dzU = A(L.dzU); gd* dvL = A(L.dvL); gd* dvU = A(L.dvU);
+    double a = 1.0;
+    auto step = [&](double z, double cs, double ts) { return (mu + z * (cs - ts)) / ts - z; };
+    for (int q = c.lane; q < D.n; q += c.width) {
+      double t = 0.0, u = 0.0;
+      if (finite_(xL[q])) { t = step(ozL[q], ox[q] - xL[q], x[q] - xL[q]); if (t < 0) a = dmin(a, -tau * ozL[q] / t); }
+      if (finite_(xU[q])) { u = step(ozU[q], xU[q] - ox[q], xU[q] - x[q]); if (u < 0) a = dmin(a, -tau * ozU[q] / u); }
+      dzL[q] = t; dzU[q] = u;
+    }
+    for (int r = c.lane; r < D.md; r += c.width) {
+      double t = step(ovL[r], os[r] - dL[r], s[r] - dL[r]), u = 0.0;
+      if (t < 0) a = dmin(a, -tau * ovL[r] / t);
+      if (finite_(dU[r])) { u = step(ovU[r], dU[r] - os[r], dU[r] - s[r]); if (u < 0) a = dmin(a, -tau * ovU[r] / u); }
+      dvL[r] = t; dvU[r] = u;
+    }
+    c.sync();
+    a = c.minv(a);
+    gd* zL = A(L.zL); gd* zU = A(L.zU); gd* vL = A(L.vL); gd* vU = A(L.vU);
+    double bmax = 0.0;
+    for (int q = c.lane; q < D.n; q += c.width) {
+      zL[q] = ozL[q] + a * dzL[q]; zU[q] = ozU[q] + a * dzU[q];
+      bmax = dmax(bmax, dmax(dabs(zL[q]), dabs(zU[q])));
+    }
+    for (int r = c.lane; r < D.md; r += c.width) {
+      vL[r] = ovL[r] + a * dvL[r]; vU[r] = ovU[r] + a * dvU[r];
+      bmax = dmax(bmax, dmax(dabs(vL[r]), dabs(vU[r])));
+    }
+    c.sync();
+    if (c.maxv(bmax) > o.bound_mult_reset_threshold) {
+      for (int q = c.lane; q < D.n; q += c.width) { zL[q] = finite_(xL[q]) ? 1.0 : 0.0; zU[q] = finite_(xU[q]) ? 1.0 : 0.0; }
+      for (int r = c.lane; r < D.md; r += c.width) { vL[r] = 1.0; vU[r] = finite_(dU[r]) ? 1.0 : 0.0; }
+    }
+    gd* yc = A(L.yc); gd* yd = A(L.yd);
+    for (int r = c.lane; r < D.mc; r += c.width) yc[r] = 0.0;
+    for (int r = c.lane; r < D.md; r += c.width) yd[r] = 0.0;
+    c.sync();
+    eval_grad_f(x, A(L.gf), sf);
+  }
+
+  // RestoRestorationPhase: n, p reset in closed form at the current x (restoration mu), zR = mu / R
+  __attribute__((noinline)) HTP_HD void resto_resto() {
+    gd* ct = A(L.ct); gd* dtv = A(L.dt);
+    eval_cons(A(L.x), ct, dtv);
+    np_init(ct, dtv, A(L.s), mu);
+    const gd* R = A(L.R);
+    gd* cc = A(L.c); gd* dd = A(L.d);
+    const int mc = D.mc, md = D.md;
+    for (int r = c.lane; r < mc; r += c.width) cc[r] = ct[r] + R[r] - R[mc + r];
+    for (int r = c.lane; r < md; r += c.width) dd[r] = dtv[r] + R[2 * mc + r] - R[2 * mc + md + r];
+    c.sync();
+  }
+
   HTP_HD HTP_FI void iterate(Result& res) {
     gd* x = A(L.x); gd* s = A(L.s);
     gd* cc = A(L.c); gd* dd = A(L.d);
-    // phi / theta of the current point are carried over from the accepted trial
-    // point (bitwise identical: x_new is computed by the same expression as x_trial)
+    // phi / theta of the current point are carried over from the accepted trial point
+    // (bitwise identical: x_new is computed by the same expression as x_trial)
     double phi_cache = 0.0, mu_cache = -1.0, theta_cache = -1.0;
-    int status = ST_MAXITER, it = 0, acc_count = 0;
+    int status = ST_MAXITER, it = 0;
+    bool rs_first = false;
     double nlp_err = 0.0;
     gd* gl = A(L.rx);
-    for (it = 0; it <= o.max_iter; ++it) {
+    gd* dx = A(L.dx); gd* ds = A(L.ds); gd* dyc = A(L.dyc); gd* dyd = A(L.dyd); gd* dR = A(L.dR);
+    const long long t_start = c.wall();
+    const double wall_limit = o.max_cpu_time > 0.0 ? o.max_cpu_time * o.wall_rate : -1.0;
+    for (;;) {
       long long tq0 = c.clock();
       grad_lag_into(gl);
       Err e0 = errors(gl, 0.0);
-      HTP_TRACE("[trace] it %d err dual=%g comp=%g prim=%g mu=%g\n", it, e0.dual, e0.comp, e0.prim_nlp, mu);
+      HTP_TRACE("[trace] it %d%s err dual=%g comp=%g prim=%g mu=%g\n", it, rs ? " R" : "", e0.dual, e0.comp, e0.prim_nlp, mu);
       nlp_err = dmax(dmax(e0.dual / e0.s_d, e0.prim_nlp), e0.comp / e0.s_c);
       const double uv = unscaled_viol();
-      if (nlp_err <= o.tol && e0.dual / sf <= o.dual_inf_tol && uv <= o.constr_viol_tol && e0.comp / sf <= o.compl_inf_tol) {
-        status = ST_SUCCESS;
-        break;
-      }
-      if (nlp_err <= o.acceptable_tol && e0.dual / sf <= o.acceptable_dual_inf_tol && uv <= o.acceptable_constr_viol_tol &&
-          e0.comp / sf <= o.acceptable_compl_inf_tol) {
-        if (++acc_count >= o.acceptable_iter) { status = ST_ACCEPTABLE; break; }
+      const double sfm = rs ? 1.0 : sf;
+      const bool optimal = nlp_err <= o.tol && e0.dual / sfm <= o.dual_inf_tol && uv <= o.constr_viol_tol &&
+                           e0.comp / sfm <= o.compl_inf_tol;
+      const bool acc_lvl = nlp_err <= o.acceptable_tol && e0.dual / sfm <= o.acceptable_dual_inf_tol &&
+                           uv <= o.acceptable_constr_viol_tol && e0.comp / sfm <= o.acceptable_compl_inf_tol;
+      if (wall_limit > 0.0 && (double)(c.wall() - t_start) > wall_limit) { status = ST_CPUTIME; break; }
+      if (rs) {
+        if (!rs_first && resto_converged()) {
+          leave_resto();
+          mu_cache = -1.0;
+          theta_cache = -1.0;
+          continue;  // the original problem resumes with this iteration number
+        }
+        if (!rs_first && (optimal || (acc_lvl && ls_.acc_count + 1 >= o.acceptable_iter))) {
+          const double ot = orig_theta_rs(cc, dd, s, A(L.R));
+          status = ot <= 1e2 * o.tol ? ST_RESTORATION : ST_INFEASIBLE;
+          if (have_acc) { copy_arr(x, A(L.ax), D.n); status = ST_ACCEPTABLE; }
+          break;
+        }
+        ls_.acc_count = acc_lvl ? ls_.acc_count + 1 : 0;
       } else {
-        acc_count = 0;
+        if (optimal) { status = ST_SUCCESS; break; }
+        if (acc_lvl) {
+          if (++ls_.acc_count >= o.acceptable_iter) { status = ST_ACCEPTABLE; break; }
+        } else {
+          ls_.acc_count = 0;
+        }
       }
-      if (it == o.max_iter) { status = ST_MAXITER; break; }
-      // monotone barrier update
+      if (it >= o.max_iter) { status = ST_MAXITER; break; }
+      rs_first = false;
+      // monotone barrier update (a tiny step forces a decrease)
+      bool stop_tiny = false;
       for (;;) {
         Err eb = errors(gl, mu);
         const double berr = dmax(dmax(eb.dual / eb.s_d, eb.prim_b), eb.comp / eb.s_c);
-        if (berr > o.kappa_eps * mu) break;
+        if (berr > o.kappa_eps * mu && !ls_.tiny_flag) break;
         const double nm = dmax(o.tol / 10.0, dmin(o.kappa_mu * mu, pow(mu, o.theta_mu)));
-        if (nm == mu) break;
+        if (nm == mu) { if (ls_.tiny_flag) stop_tiny = true; break; }
         mu = nm;
         tau = dmax(o.tau_min, 1.0 - mu);
         nfilt = 0;
+        ls_.tiny_flag = 0;
+        if (rs) {  // the restoration objective depends on mu (eta = sqrt(mu))
+          eta = o.resto_proximity_weight * sqrt(mu);
+          eval_grad_f_rs(x, A(L.gf));
+          grad_lag_into(gl);
+        }
       }
+      if (stop_tiny) { status = ST_TINYSTEP; break; }
+      ls_.tiny_flag = 0;
       cyc[5] += c.clock() - tq0;
-      // Newton rhs: rx = grad_barrier + J'y ; rs = gbs - yd ; rc = c ; rd = d - s  (negated below)
-      gd* gbx = A(L.sx);   // scratch for barrier gradient
-      gd* gbs = A(L.ss);
-      grad_barrier(mu, gbx, gbs);
-      gd* rx = A(L.xt);    // use xt as rhs storage (x part), rebuilt below
-      gd* rs = A(L.rs); gd* rc = A(L.rc); gd* rd = A(L.rd);
-      {
-        const gd* gf = A(L.gf);
-        const gd* yd = A(L.yd);
-        {
-          double a_[SW_U], b_[SW_U], g_[SW_U];
-          sweep(D.n, [&](int q, int k) { a_[k] = gl[q]; b_[k] = gf[q]; g_[k] = gbx[q]; },
-                [&](int q, int k) { rx[q] = -(a_[k] - b_[k] + g_[k]); });
-        }
-        {
-          double a_[SW_U], b_[SW_U], d_[SW_U], s_[SW_U];
-          sweep(D.md, [&](int r, int k) { a_[k] = gbs[r]; b_[k] = yd[r]; d_[k] = dd[r]; s_[k] = s[r]; },
-                [&](int r, int k) { rs[r] = -(a_[k] - b_[k]); rd[r] = -(d_[k] - s_[k]); });
-        }
-        {
-          double a_[SW_U];
-          sweep(D.mc, [&](int r, int k) { a_[k] = cc[r]; }, [&](int r, int k) { rc[r] = -a_[k]; });
-        }
-        c.sync();
+      // Newton step: rx (in xt), rs, rc, rd[, rRx]; barrier gradient in sx, ss
+      build_newton_rhs(gl);
+      double dw = 0.0, dc = 0.0;
+      const bool have_step = factor_ic(dw, dc);
+      if (!have_step) {
+        ls_.fallback = 1;
+      } else {
+        if (dw > 0.0) dw_last = dw;
+        HTP_TRACE("[trace] factored dw=%g\n", dw);
+        kkt_solve(false, dw, dc, A(L.xt), A(L.rs), A(L.rc), A(L.rd), dx, ds, dyc, dyd, A(L.rRx), dR);
       }
-      double dw, dc;
-      if (!factor_ic(dw, dc)) { status = ST_STEPFAIL; break; }
-      if (dw > 0.0) dw_last = dw;
-      gd* dx = A(L.dx); gd* ds = A(L.ds); gd* dyc = A(L.dyc); gd* dyd = A(L.dyd);
-      HTP_TRACE("[trace] factored dw=%g\n", dw);
-      kkt_solve(false, dw, dc, rx, rs, rc, rd, dx, ds, dyc, dyd);
-      HTP_TRACE("[trace] solved\n");
-      // line search
+      // ---- line search (IpBacktrackingLineSearch::FindAcceptableTrialPoint)
       long long tls = c.clock();
-      const double phi = (mu_cache == mu) ? phi_cache : barrier(x, s, mu);
-      const double theta = (theta_cache >= 0.0) ? theta_cache : theta_of(cc, dd, s);
-      double gBD = 0.0;
-      {
-        double a_[SW_U], b_[SW_U];
-        sweep(D.n, [&](int q, int k) { a_[k] = gbx[q]; b_[k] = dx[q]; }, [&](int, int k) { gBD += a_[k] * b_[k]; });
-        sweep(D.md, [&](int r, int k) { a_[k] = gbs[r]; b_[k] = ds[r]; }, [&](int, int k) { gBD += a_[k] * b_[k]; });
+      if (!rs && acc_lvl) { copy_arr(A(L.ax), x, D.n); have_acc = true; }
+      if (ls_.last_mu != mu) { ls_.in_wd = 0; ls_.wd_short = 0; ls_.last_mu = mu; }
+      double phi = (mu_cache == mu) ? phi_cache : barrier(x, s, A(L.R), mu, rs);
+      double theta = (theta_cache >= 0.0) ? theta_cache : theta_of(cc, dd, s);
+      bool goto_resto = ls_.fallback != 0;
+      ls_.fallback = 0;
+      const double gbd = goto_resto ? 0.0 : newton_gbd(dx, ds, dR);
+      copy_arr(A(L.sx), A(L.xt), D.n);  // keep the Newton rhs (x part) for second-order corrections
+      double rth = theta, rph = phi, rgbd = gbd;
+      if (ls_.in_wd) { rth = ls_.wd_th; rph = ls_.wd_ph; rgbd = ls_.wd_gbd; }
+      bool accept = false;
+      int n_steps = 0;
+      double a_primal = 0.0, a_test = 0.0, ph_t = 0.0, th_t = 0.0;
+      double cdw = dw, cdc = dc;
+      bool tiny = !goto_resto && detect_tiny_step(dx, ds, dyc, dyd, dR);
+      if (ls_.in_wd && (goto_resto || tiny)) {
+        stop_watchdog();
+        copy_arr(A(L.sx), A(L.xt), D.n);
+        theta = rth; phi = rph; cdw = ls_.wd_dw; cdc = ls_.wd_dc;
+        goto_resto = tiny = false;
       }
-      gBD = c.sum(gBD);
-      const double alpha_max = frac_primal(dx, ds);
-      double a_min = o.gamma_theta;
-      if (gBD < 0) {
-        a_min = dmin(o.gamma_theta, o.gamma_phi * theta / (-gBD));
-        if (theta <= theta_min) a_min = dmin(a_min, o.delta * pow(theta, o.s_theta) / pow(-gBD, o.s_phi));
+      if (o.watchdog_shortened_iter_trigger > 0 && !ls_.in_wd && !goto_resto && !tiny && !ls_.in_soft &&
+          ls_.wd_short >= o.watchdog_shortened_iter_trigger)
+        start_watchdog(theta, phi, gbd, dw, dc);
+      if (tiny) {
+        a_primal = frac_primal(dx, ds, dR);
+        set_trial(a_primal, dx, ds, dR);
+        trial_values(A(L.xt), A(L.st), A(L.Rt), th_t, ph_t);
+        if (ls_.tiny_last) ls_.tiny_flag = 1;
+        ls_.tiny_last = 1;
+        accept = true;
+      } else {
+        ls_.tiny_last = 0;
       }
-      a_min *= o.alpha_min_frac;
-      auto is_ftype = [&](double a) { return gBD < 0 && a * pow(-gBD, o.s_phi) > o.delta * pow(theta, o.s_theta); };
-      // keep the Newton rhs (x part) for SOC solves: copy into sx after gbx is consumed
-      gd* rxk = A(L.sx);
-      {
-        double a_[SW_U];
-        sweep(D.n, [&](int q, int k) { a_[k] = rx[q]; }, [&](int q, int k) { rxk[q] = a_[k]; });
-      }
-      c.sync();
-      gd* xt = A(L.xt); gd* st = A(L.st);
-      double alpha = alpha_max, a_primal = alpha, a_test = alpha, th_t = 0, ph_t = 0, th_acc = 0;
-      bool accepted = false, soc_used = false, first = true;
-      while (alpha >= a_min) {
-        {
-          double a_[SW_U], b_[SW_U];
-          sweep(D.n, [&](int q, int k) { a_[k] = x[q]; b_[k] = dx[q]; }, [&](int q, int k) { xt[q] = a_[k] + alpha * b_[k]; });
-          sweep(D.md, [&](int r, int k) { a_[k] = s[r]; b_[k] = ds[r]; }, [&](int r, int k) { st[r] = a_[k] + alpha * b_[k]; });
-        }
-        c.sync();
-        if (acceptable(alpha, xt, st, phi, theta, gBD, is_ftype(alpha), th_t, ph_t)) {
-          accepted = true; a_primal = alpha; a_test = alpha; th_acc = th_t;
-          break;
-        }
-        HTP_TRACE("[trace]   ls alpha=%.17g th_t=%.17g ph_t=%.17g (theta=%.17g phi=%.17g gBD=%.17g amax=%.17g)\n", alpha, th_t, ph_t, theta, phi, gBD, alpha_max);
-        if (first && th_t >= theta && o.max_soc > 0) {
-          gd* csoc = A(L.csoc); gd* dsoc = A(L.dsoc);
-          const gd* ct = A(L.ct); const gd* dtv = A(L.dt);
-          HTP_UNROLL
-          for (int r = c.lane; r < D.mc; r += c.width) csoc[r] = alpha * cc[r] + ct[r];
-          HTP_UNROLL
-          for (int r = c.lane; r < D.md; r += c.width) dsoc[r] = alpha * (dd[r] - s[r]) + (dtv[r] - st[r]);
-          c.sync();
-          double th_old = theta;
-          gd* sx = A(L.dzL);  // temporaries (dz arrays are recomputed after acceptance)
-          gd* ss_ = A(L.dvL); gd* syc = A(L.syc); gd* syd = A(L.syd);
-          gd* nrc = A(L.ct); gd* nrd = A(L.dt);
-          for (int k = 0; k < o.max_soc; ++k) {
-            HTP_UNROLL
-            for (int r = c.lane; r < D.mc; r += c.width) nrc[r] = -csoc[r];
-            HTP_UNROLL
-            for (int r = c.lane; r < D.md; r += c.width) nrd[r] = -dsoc[r];
-            c.sync();
-            kkt_solve(false, dw, dc, rxk, rs, nrc, nrd, sx, ss_, syc, syd);
-            const double a_soc = frac_primal(sx, ss_);
-            HTP_UNROLL
-            for (int q = c.lane; q < D.n; q += c.width) xt[q] = x[q] + a_soc * sx[q];
-            HTP_UNROLL
-            for (int r = c.lane; r < D.md; r += c.width) st[r] = s[r] + a_soc * ss_[r];
-            c.sync();
-            double th_soc, ph_soc;
-            if (acceptable(alpha, xt, st, phi, theta, gBD, is_ftype(alpha), th_soc, ph_soc)) {
-              accepted = true; soc_used = true; a_primal = a_soc; a_test = alpha; ph_t = ph_soc; th_acc = th_soc;
-              HTP_UNROLL
-              for (int q = c.lane; q < D.n; q += c.width) dx[q] = sx[q];
-              HTP_UNROLL
-              for (int r = c.lane; r < D.md; r += c.width) { ds[r] = ss_[r]; dyd[r] = syd[r]; }
-              HTP_UNROLL
-              for (int r = c.lane; r < D.mc; r += c.width) dyc[r] = syc[r];
-              c.sync();
+      int soft = 0;
+      if (!goto_resto && !tiny) {
+        if (ls_.in_soft) {
+          if (++ls_.soft_cnt > o.max_soft_resto_iters) {
+            accept = false;
+          } else {
+            soft = try_soft_resto_step(rth, rph, rgbd, gl);
+            if (soft == 2) { ls_.in_soft = 0; ls_.soft_cnt = 0; }
+          }
+        } else {
+          bool skip = false;
+          for (;;) {
+            accept = backtrack(rth, rph, rgbd, skip, n_steps, a_primal, a_test, ph_t, th_t, cdw, cdc);
+            if (ls_.in_wd) {
+              if (accept) { ls_.in_wd = 0; break; }
+              if (++ls_.wd_trial > o.watchdog_trial_iter_max) {
+                stop_watchdog();
+                copy_arr(A(L.sx), A(L.xt), D.n);
+                rth = ls_.wd_th; rph = ls_.wd_ph; rgbd = ls_.wd_gbd;
+                theta = rth; phi = rph; cdw = ls_.wd_dw; cdc = ls_.wd_dc;
+                skip = true;
+                continue;
+              }
+              accept = true;  // the watchdog takes the full step unchecked
               break;
             }
-            if (th_soc > o.kappa_soc * th_old) break;
-            th_old = th_soc;
-            const gd* ct2 = A(L.ct); const gd* dt2 = A(L.dt);
-            HTP_UNROLL
-            for (int r = c.lane; r < D.mc; r += c.width) csoc[r] = a_soc * csoc[r] + ct2[r];
-            HTP_UNROLL
-            for (int r = c.lane; r < D.md; r += c.width) dsoc[r] = a_soc * dsoc[r] + (dt2[r] - st[r]);
-            c.sync();
+            break;
           }
-          if (accepted) break;
         }
-        first = false;
-        alpha *= 0.5;
+      }
+      if (!soft && !accept) {
+        if (!ls_.in_soft && o.soft_resto_pderror_reduction_factor > 0.0 && !goto_resto) {
+          filter_add(rth, rph);  // PrepareRestoPhaseStart
+          soft = try_soft_resto_step(rth, rph, rgbd, gl);
+          if (soft == 1) ls_.in_soft = 1;
+        } else if (!ls_.in_soft) {
+          filter_add(rth, rph);
+        }
+        if (!soft) {
+          cyc[6] += c.clock() - tls;
+          if (theta <= 1e-2 * o.tol) {  // restoration phase called at an almost feasible point
+            status = have_acc ? ST_ACCEPTABLE : ST_RESTORATION;
+            if (have_acc) copy_arr(x, A(L.ax), D.n);
+            break;
+          }
+          ls_.in_soft = 0; ls_.soft_cnt = 0; ls_.wd_short = 0; ls_.cnt_filter_rej = 0;
+          if (rs) {
+            resto_resto();
+          } else {
+            enter_resto(rth, rph, rgbd);
+            rs_first = true;
+          }
+          mu_cache = -1.0;
+          theta_cache = -1.0;
+          ++it;
+          continue;
+        }
       }
       cyc[6] += c.clock() - tls;
-      if (!accepted) { status = ST_RESTORATION; break; }
-      (void)soc_used;
-      // filter augmentation (uses the accepted trial's barrier value)
-      if (!(is_ftype(a_test) && cmp_le(ph_t - phi, o.eta_phi * a_test * gBD, phi))) {
-        c.sync();
-        if (c.lane == 0) {
-          if (nfilt < FMAX) { f_th[nfilt] = (1 - o.gamma_theta) * theta; f_ph[nfilt] = phi - o.gamma_phi * theta; }
-          else { for (int k = 1; k < FMAX; ++k) { f_th[k - 1] = f_th[k]; f_ph[k - 1] = f_ph[k]; }
-                 f_th[FMAX - 1] = (1 - o.gamma_theta) * theta; f_ph[FMAX - 1] = phi - o.gamma_phi * theta; }
-        }
-        if (nfilt < FMAX) ++nfilt;
-        c.sync();
+      if (soft) {
+        mu_cache = -1.0;
+        theta_cache = -1.0;
+        ++it;
+        continue;
       }
+      HTP_TRACE("[trace]   acc it=%d a=%.17g th_t=%.17g ph_t=%.17g ref_th=%.17g ref_ph=%.17g n_steps=%d\n", it, a_primal, th_t, ph_t, rth, rph, n_steps);
       long long tup = c.clock();
-      const double a_dual = dual_steps(dx, ds);
-      {
-        gd* zL = A(L.zL); gd* zU = A(L.zU); gd* vL = A(L.vL); gd* vU = A(L.vU);
-        gd* yc = A(L.yc); gd* yd = A(L.yd);
-        const gd* dzL = A(L.dzL); const gd* dzU = A(L.dzU);
-        const gd* dvL = A(L.dvL); const gd* dvU = A(L.dvU);
-        const gd* xL = A(L.xL); const gd* xU = A(L.xU);
-        const gd* dL = A(L.dL); const gd* dU = A(L.dU);
-        const double ks = o.kappa_sigma;
-        {
-          double x_[SW_U], d_[SW_U], xl_[SW_U], xu_[SW_U], zl_[SW_U], zu_[SW_U], dzl_[SW_U], dzu_[SW_U];
-          sweep(D.n, [&](int q, int k) { x_[k] = x[q]; d_[k] = dx[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; zl_[k] = zL[q];
-                                          zu_[k] = zU[q]; dzl_[k] = dzL[q]; dzu_[k] = dzU[q]; },
-                [&](int q, int k) {
-                  const double xn = x_[k] + a_primal * d_[k];
-                  x[q] = xn;
-                  if (finite_(xl_[k])) { const double z = zl_[k] + a_dual * dzl_[k], v = xn - xl_[k]; zL[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
-                  if (finite_(xu_[k])) { const double z = zu_[k] + a_dual * dzu_[k], v = xu_[k] - xn; zU[q] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
-                });
-        }
-        {
-          double s_[SW_U], d_[SW_U], y_[SW_U], dy_[SW_U], vl_[SW_U], dvl_[SW_U], dl_[SW_U], vu_[SW_U], dvu_[SW_U], du_[SW_U];
-          sweep(D.md, [&](int r, int k) { s_[k] = s[r]; d_[k] = ds[r]; y_[k] = yd[r]; dy_[k] = dyd[r]; vl_[k] = vL[r];
-                                           dvl_[k] = dvL[r]; dl_[k] = dL[r]; vu_[k] = vU[r]; dvu_[k] = dvU[r]; du_[k] = dU[r]; },
-                [&](int r, int k) {
-                  const double sn = s_[k] + a_primal * d_[k];
-                  s[r] = sn;
-                  yd[r] = y_[k] + a_primal * dy_[k];
-                  { const double z = vl_[k] + a_dual * dvl_[k], v = sn - dl_[k]; vL[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
-                  if (finite_(du_[k])) { const double z = vu_[k] + a_dual * dvu_[k], v = du_[k] - sn; vU[r] = dmax(dmin(z, ks * mu / v), mu / (ks * v)); }
-                });
-        }
-        {
-          double y_[SW_U], dy_[SW_U];
-          sweep(D.mc, [&](int r, int k) { y_[k] = yc[r]; dy_[k] = dyc[r]; },
-                [&](int r, int k) { yc[r] = y_[k] + a_primal * dy_[k]; });
-        }
-        c.sync();
-      }
-      {  // constraint values at the new point = those of the accepted trial point
-        const gd* ct = A(L.ct); const gd* dtv = A(L.dt);
-        double a_[SW_U];
-        sweep(D.mc, [&](int r, int k) { a_[k] = ct[r]; }, [&](int r, int k) { cc[r] = a_[k]; });
-        sweep(D.md, [&](int r, int k) { a_[k] = dtv[r]; }, [&](int r, int k) { dd[r] = a_[k]; });
-      }
+      const double a_dual = dual_steps(dx, ds, dR);
+      accept_step(a_primal, a_dual, dx, ds, dyc, dyd, dR);
+      if (n_steps == 0) ls_.wd_short = 0;
+      if (n_steps > 0) ++ls_.wd_short;
       phi_cache = ph_t;
       mu_cache = mu;
-      theta_cache = th_acc;
-      c.sync();
-      eval_grad_f(x, A(L.gf), sf);
+      theta_cache = th_t;
+      eval_grad_mode(x);
       cyc[7] += c.clock() - tup;
+      ++it;
     }
     // honor_original_bounds: project into the unrelaxed bounds
     project_original_bounds();
@@ -3172,6 +4007,7 @@ struct ObcaSolver {
       res.status = status;
       res.iters = it;
       res.n_factor = n_factor;
+      res.n_resto = n_resto;
       res.objective = fobj;
       res.final_mu = mu;
       res.nlp_error = nlp_err;

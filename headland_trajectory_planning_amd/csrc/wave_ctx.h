@@ -2,6 +2,7 @@
 // gfx950 (DevWave), or a single serial lane for the test-only host build
 // (HostLane, tests/ only -- never a product fallback).
 #pragma once
+#include <chrono>
 #include <cmath>
 
 namespace htp {
@@ -57,6 +58,8 @@ struct DevWave {
   __device__ __forceinline__ int uniform_i(int v) const { return __builtin_amdgcn_readfirstlane(v); }
   __device__ __forceinline__ double bcast(double v, int src) const { return __shfl(v, src, 64); }
   __device__ __forceinline__ long long clock() const { return (long long)__builtin_amdgcn_s_memtime(); }
+  // constant-rate wall clock (hipDeviceAttributeWallClockRate ticks/s), for max_cpu_time
+  __device__ __forceinline__ long long wall() const { return (long long)wall_clock64(); }
 };
 #endif
 
@@ -79,6 +82,10 @@ struct HostLane {
   double uniform(double v) const { return v; }
   int uniform_i(int v) const { return v; }
   long long clock() const { return 0; }
+  long long wall() const {  // ns (Options::wall_rate = 1e9 on the host builds)
+    return (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
 };
 
 }  // namespace htp

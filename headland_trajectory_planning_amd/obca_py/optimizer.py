@@ -238,9 +238,10 @@ class OBCAOptimizer(object):
 
     # ------------------------------------------------------------- solve
     def solve(self, max_cpu_time=20, verbose: bool = False) -> Tuple[bool, Dict]:
-        """optimizer.py:475-571.  max_cpu_time is accepted for API parity; the
-        iteration limit is IPOPT's max_iter (3000)."""
-        (success, solution), = solve_batch([self], verbose=verbose)
+        """optimizer.py:475-571.  max_cpu_time (IPOPT option, optimizer.py:486) limits
+        the solve's time on the device clock; a solve that exceeds it stops with
+        "Maximum_CpuTime_Exceeded" (success False)."""
+        (success, solution), = solve_batch([self], verbose=verbose, max_cpu_time=max_cpu_time)
         return success, solution
 
     @staticmethod
@@ -274,12 +275,14 @@ class OBCAOptimizer(object):
         print("slack cost: ", slack_cost)
 
 
-def solve_batch(optimizers: List[OBCAOptimizer], verbose: bool = False, device: int = None):
-    """Solve many OBCAOptimizer problems in one HIP launch -> [(success, solution)]."""
+def solve_batch(optimizers: List[OBCAOptimizer], verbose: bool = False, device: int = None, max_cpu_time=None):
+    """Solve many OBCAOptimizer problems in one HIP launch -> [(success, solution)].
+    max_cpu_time (seconds, per problem, device clock; None/<= 0: no limit)."""
     if not optimizers:
         return []
     dev = optimizers[0].device if device is None else device
     ctx = _context(dev)
+    ctx.set_option("max_cpu_time", float(max_cpu_time) if max_cpu_time else 0.0)
     pk = _native.PackedBatch([o.instance() for o in optimizers])
     res = ctx.solve(pk)
     out = []

@@ -174,6 +174,8 @@ def solve_batch(optimizers: List[OBCAOptimizer], device=0):
     if not optimizers:
         return
     packed = _native.PointsPackedBatch([o.instance() for o in optimizers])
-    res = _context(device).solve_points(packed)
+    ctx = _context(device)
+    ctx.set_option("max_cpu_time", 0.0)  # optimizer_points.py:163 sets no CPU-time limit
+    res = ctx.solve_points(packed)
     for k, o in enumerate(optimizers):
         o._take(res, k)

@@ -37,9 +37,12 @@ enum {
   HTP_STATUS_SUCCESS = 0,            /* IPOPT "Solve_Succeeded" */
   HTP_STATUS_ACCEPTABLE = 1,         /* "Solved_To_Acceptable_Level" */
   HTP_STATUS_MAX_ITER = 2,           /* "Maximum_Iterations_Exceeded" */
-  HTP_STATUS_RESTORATION_FAILED = 3, /* line search failed (restoration phase not restated) */
+  HTP_STATUS_RESTORATION_FAILED = 3, /* "Restoration_Failed" */
   HTP_STATUS_STEP_FAILED = 4,        /* "Error_In_Step_Computation" */
-  HTP_STATUS_BAD_INPUT = 5
+  HTP_STATUS_BAD_INPUT = 5,          /* "Invalid_Problem_Definition" */
+  HTP_STATUS_CPUTIME = 6,            /* "Maximum_CpuTime_Exceeded" (option max_cpu_time, device clock) */
+  HTP_STATUS_INFEASIBLE = 7,         /* "Infeasible_Problem_Detected" (restoration converged, infeasible) */
+  HTP_STATUS_TINY_STEP = 8           /* "Search_Direction_Becomes_Too_Small" */
 };
 
 typedef struct htp_ctx htp_ctx;
@@ -68,6 +71,7 @@ typedef struct {
   int32_t* iterations;  /* [batch] IPM iterations */
   int32_t* n_factor;    /* [batch] KKT factorizations (inertia-correction retries included) */
   double* nlp_error;    /* [batch] final scaled NLP error */
+  int32_t* n_resto;     /* nullable [batch] feasibility restoration phases entered */
 } htp_obca_result;
 
 /* Sizes of one problem (n_var, n_eq, n_ineq as printed by optimizer.py:490-498)
@@ -79,7 +83,8 @@ int htp_obca_sizes(int32_t N, int32_t M, int32_t K, int32_t time_opt, const int3
 htp_ctx* htp_create(int32_t device);
 void htp_destroy(htp_ctx* ctx);
 const char* htp_last_error(htp_ctx* ctx);
-/* IPOPT option override by name (e.g. "tol", "max_iter"); 0 = OK */
+/* IPOPT option override by name (e.g. "tol", "max_iter", "max_cpu_time" = seconds per problem on the
+ * device wall clock, <= 0 off); 0 = OK */
 int htp_set_option(htp_ctx* ctx, const char* name, double value);
 
 /* Host buffers in, host buffers out (synchronous). */

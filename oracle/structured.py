@@ -83,8 +83,11 @@ class StructuredKKT:
         nlp = self.nlp
         Wm, Jc, Jd = Wm.tocsr(), Jc.tocsr(), Jd.tocsr()
         n, mc, md = Wm.shape[0], Jc.shape[0], Jd.shape[0]
+        # dc: scalar, or per row [equality rows (E order), inequality rows] (restoration phase)
+        dcv = np.broadcast_to(np.asarray(dc, dtype=float), (mc + md,))
+        dcc, dcd = dcv[:mc], dcv[mc:]
         Ds = Ss + dw
-        Ed = 1.0 / Ds + dc
+        Ed = 1.0 / Ds + dcd
         import scipy.sparse as sp
         Hb = (Wm + sp.diags(Sx + dw) + Jd.T @ sp.diags(1.0 / Ed) @ Jd).tocsr()
         pos, neg, zer = md, md, 0
@@ -111,7 +114,7 @@ class StructuredKKT:
             Cz = jsub(rows, z)
             K[nz:, :nz] = Cz
             K[:nz, nz:] = Cz.T
-            K[nz:, nz:] = -dc * np.eye(nr)
+            K[nz:, nz:] = -np.diag(dcc[rows])
             B = np.vstack([hsub(z, p), jsub(rows, p)])
             a, b_, c_ = _eig_inertia(K)
             pos, neg, zer = pos + a, neg + b_, zer + c_
@@ -129,7 +132,7 @@ class StructuredKKT:
             v, r = self.stage_vars[i], self.stage_rows[i]
             nv, nr = v.size, r.size
             K = np.zeros((nr + nv, nr + nv))
-            K[:nr, :nr] = -dc * np.eye(nr)
+            K[:nr, :nr] = -np.diag(dcc[r])
             Jr = jsub(r, v)
             K[:nr, nr:] = Jr
             K[nr:, :nr] = Jr.T

@@ -1,0 +1,51 @@
+"""Generate the full-size OBCA parity fixtures (tests/golden/obca_full/*.npz).
+
+TEST INFRASTRUCTURE: the oracle (oracle/ipm.py IPOPT restatement with the
+structured KKT of oracle/structured.py) solves selected problems of the
+BASELINE configs A-E (synth.make_instance, the same Philox-seeded workload as
+bench.py) on the CPU; each fixture stores the state trajectory (5N), the
+objective, the status, the iteration count and the number of restoration
+phases.  tests/test_gpu_obca.py compares the HIP solver against them (the
+oracle needs minutes to hours per full-size problem, too slow to run inside a
+GPU test).  Several pids are problems whose line search fails and that need
+IPOPT's feasibility restoration (D 33/971, C 47/66, E 12).
+
+    python tests/golden/make_obca_golden.py [CFG:PID ...]
+"""
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "tests", "golden", "obca_full")
+
+CASES = ["A:0", "A:1", "A:2", "D:0", "D:33", "D:971", "C:0", "C:47", "C:66", "E:0", "E:1", "E:12"]
+
+
+def run(case):
+    from headland_trajectory_planning_amd import synth
+    from oracle.ipm import IpoptRestatement
+    from oracle.nlp import ObcaNLP
+    from oracle.structured import StructuredKKT
+    cfg, pid = case.split(":")
+    pid = int(pid)
+    _, N, M, imp = synth.CONFIGS[cfg]
+    nlp = ObcaNLP(synth.make_instance(pid, N=N, M=M, implement=imp))
+    t = time.time()
+    r = IpoptRestatement(nlp, kkt=StructuredKKT(nlp)).solve()
+    dt = time.time() - t
+    np.savez(os.path.join(OUT, f"{cfg}{pid}.npz"), states=r["x"][:5 * N], f=r["f"], status=r["status"],
+             iters=r["iters"], n_resto=r["n_resto"], N=N, M=M, implement=imp, seconds=dt)
+    return f"{case} {r['status_str']} iters={r['iters']} n_resto={r['n_resto']} f={r['f']:.12g} ({dt:.0f} s)"
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    cases = sys.argv[1:] or CASES
+    with mp.Pool(min(8, len(cases))) as pool:
+        for line in pool.imap_unordered(run, cases):
+            print(line, flush=True)

@@ -1,11 +1,19 @@
 """GPU parity: the HIP solver (libhtp.so via the C ABI) against the oracle.
 
 * small shapes: state trajectories vs the dense IPOPT restatement (oracle/ipm.py)
-  within 1e-4 (north_star tolerance), identical solver status;
-* full config shapes: size-independent properties -- KKT conditions of the
-  oracle NLP at the returned point, batch-composition invariance and
-  determinism.
+  within 1e-4 (north_star tolerance), identical solver status and iteration
+  count -- the chosen pids include problems whose filter line search fails and
+  that IPOPT's feasibility restoration phase recovers;
+* full BASELINE shapes (configs A-E): states within 1e-4, status, iteration
+  count and restoration count vs fixtures the oracle made on the CPU
+  (tests/golden/make_obca_golden.py), the former line-search failures among them;
+* full config batches: success rate, primal feasibility and a stationarity
+  (dual-residual) check of the oracle NLP at the returned point, batch-composition
+  invariance and determinism.
 """
+import glob
+import os
+
 import numpy as np
 import pytest
 
@@ -16,6 +24,11 @@ from oracle.nlp import ObcaNLP
 pytestmark = pytest.mark.gpu
 
 STATE_TOL = 1e-4
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "obca_full")
+
+# (N, M, implement, time-opt, pids): pids with restoration phases on every shape
+SMALL = [(12, 2, "mower", True, (0, 3, 5)), (10, 3, "none", True, (0, 1)), (12, 2, "none", False, (1, 2, 5)),
+         (8, 1, "pruner", True, (2, 4, 5))]
 
 
 @pytest.fixture(scope="module")
@@ -23,19 +36,41 @@ def ctx():
     return _native.Context(0)
 
 
-@pytest.mark.parametrize("N,M,imp,topt", [(12, 2, "mower", True), (10, 3, "none", True), (12, 2, "none", False),
-                                          (8, 1, "pruner", True)])
-def test_parity_small_vs_oracle(ctx, N, M, imp, topt):
+@pytest.mark.parametrize("N,M,imp,topt,pids", SMALL)
+def test_parity_small_vs_oracle(ctx, N, M, imp, topt, pids):
     W = np.diag([10.0, 0.1 if topt else 0.0])
-    insts = [synth.make_instance(pid, N=N, M=M, implement=imp, W=W) for pid in range(3)]
+    insts = [synth.make_instance(pid, N=N, M=M, implement=imp, W=W) for pid in pids]
     res = ctx.solve(_native.PackedBatch(insts))
     for k, inst in enumerate(insts):
-        nlp = ObcaNLP(inst)
-        ref = IpoptRestatement(nlp).solve()
-        assert res.status[k] == ref["status"]
+        ref = IpoptRestatement(ObcaNLP(inst)).solve()
+        assert res.status[k] == ref["status"], (pids[k], res.status[k], ref["status"])
+        assert res.status[k] in (0, 1)
+        assert res.iterations[k] == ref["iters"] and res.n_resto[k] == ref["n_resto"]
         xs, rs = res.x[k, :5 * N], ref["x"][:5 * N]
         assert np.max(np.abs(xs - rs)) <= STATE_TOL
+        assert np.max(np.abs(res.x[k] - ref["x"])) <= 1e-3          # multipliers mu, lambda, tau, slack too
         assert abs(res.objective[k] - ref["f"]) <= 1e-6 * max(1.0, abs(ref["f"]))
+
+
+def _golden():
+    out = []
+    for f in sorted(glob.glob(os.path.join(GOLD, "*.npz"))):
+        name = os.path.basename(f)[:-4]
+        out.append((name[0], int(name[1:]), f))
+    return out
+
+
+@pytest.mark.parametrize("cfg,pid,path", _golden(), ids=lambda v: str(v) if not str(v).endswith(".npz") else "")
+def test_full_config_parity_vs_oracle_fixtures(ctx, cfg, pid, path):
+    g = np.load(path)
+    _, N, M, imp = synth.CONFIGS[cfg]
+    assert int(g["N"]) == N
+    res = ctx.solve(_native.PackedBatch([synth.make_instance(pid, N=N, M=M, implement=imp)]))
+    assert res.status[0] == int(g["status"]) and res.status[0] in (0, 1), (res.status[0], int(g["status"]))
+    assert np.max(np.abs(res.x[0, :5 * N] - g["states"])) <= STATE_TOL
+    assert abs(res.objective[0] - float(g["f"])) <= 1e-6 * max(1.0, abs(float(g["f"])))
+    # the restoration phases the oracle needed are taken on the device too
+    assert (res.n_resto[0] > 0) == (int(g["n_resto"]) > 0)
 
 
 def _kkt_residuals(nlp, x):
@@ -47,23 +82,55 @@ def _kkt_residuals(nlp, x):
     return viol.max(), bnd.max()
 
 
-@pytest.mark.parametrize("cfg", ["B", "C", "E"])
-def test_full_config_properties(ctx, cfg):
+def _stationarity(nlp, x, tol_act=1e-3):
+    """Dual residual of the oracle NLP at x: least-squares multipliers of the
+    equality and active inequality rows / bounds, relative to |grad f|."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    g = nlp.cons(x)
+    eq = nlp.g_L == nlp.g_U
+    act = eq | (np.abs(g - nlp.g_L) <= tol_act) | (np.abs(g - nlp.g_U) <= tol_act)
+    J = nlp.jac(x).tocsr()[act]
+    bl = np.isfinite(nlp.x_L) & (np.abs(x - nlp.x_L) <= tol_act)
+    bu = np.isfinite(nlp.x_U) & (np.abs(x - nlp.x_U) <= tol_act)
+    E = sp.identity(nlp.n, format="csr")
+    A = sp.vstack([J, E[bl], E[bu]]).T.tocsr()
+    gf = nlp.grad_f(x)
+    y = spla.lsqr(A, -gf, atol=1e-14, btol=1e-14, iter_lim=20000)[0]
+    return np.max(np.abs(gf + A @ y)) / max(1.0, np.max(np.abs(gf)))
+
+
+@pytest.mark.parametrize("cfg,nprob,min_ok", [("B", 64, 0.98), ("C", 64, 0.98), ("E", 16, 0.85)])
+def test_full_config_properties(ctx, cfg, nprob, min_ok):
     _, N, M, imp = synth.CONFIGS[cfg]
-    insts = [synth.make_instance(pid, N=N, M=M, implement=imp) for pid in range(64 if cfg != "E" else 16)]
+    insts = [synth.make_instance(pid, N=N, M=M, implement=imp) for pid in range(nprob)]
     pk = _native.PackedBatch(insts)
     res = ctx.solve(pk)
     ok = np.isin(res.status, [0, 1])
-    # the rest are line-search failures where IPOPT would enter its restoration phase (not restated);
-    # the long-horizon pruner config E has more of them
-    assert ok.mean() >= (0.9 if cfg != "E" else 0.75), np.bincount(res.status)
-    for k in np.where(ok)[0][:8]:
+    # config E (N=160, 12 obstacles, pruner) keeps a few long orig/restoration cycles that end at
+    # max_iter or in a local infeasibility (the oracle shows the same: oracle/ipm.py, DESIGN.md 3.1c)
+    assert ok.mean() >= min_ok, np.bincount(res.status)
+    for k in np.where(ok)[0][:6]:
         nlp = ObcaNLP(insts[k])
         cv, bv = _kkt_residuals(nlp, res.x[k])
         assert cv <= 1e-4 and bv <= 1e-12, (k, cv, bv)
+        if cfg != "E":
+            assert _stationarity(nlp, res.x[k]) <= 1e-5, k
     # batch-composition invariance: problem 5 alone == problem 5 inside the batch
     solo = ctx.solve(_native.PackedBatch([insts[5]]))
     assert np.array_equal(solo.x[0], res.x[5])
     # determinism
     again = ctx.solve(pk)
     assert np.array_equal(again.x, res.x)
+
+
+def test_max_cpu_time_stops_the_solve(ctx):
+    """optimizer.py:486 passes max_cpu_time to IPOPT; the device clock limit stops every problem."""
+    insts = [synth.make_instance(pid, N=80, M=6) for pid in range(8)]
+    ctx.set_option("max_cpu_time", 1e-6)
+    try:
+        res = ctx.solve(_native.PackedBatch(insts))
+    finally:
+        ctx.set_option("max_cpu_time", 0.0)
+    assert np.all(res.status == 6), res.status                         # Maximum_CpuTime_Exceeded
+    assert np.all(res.iterations <= 1)
