@@ -21,15 +21,28 @@ def ctx():
     return _native.Context(0)
 
 
-def _check(g, h, k, n_states):
-    """Same status; converged solves agree on the states within 1e-6 and on every
-    variable (lambda included) within 1e-4.  Line-search failures (IPOPT would
-    enter its restoration phase, not restated) only need the same status: the
-    failing iterate is not a solution and amplifies last-bit differences."""
+def _feasible(inst, x, tol=1e-6):
+    nlp = PointNLP(inst)
+    c = nlp.cons(x)
+    eq = nlp.g_L == nlp.g_U
+    return (np.max(np.abs(c[eq] - nlp.g_L[eq])) < tol and np.all(c[~eq] >= nlp.g_L[~eq] - tol)
+            and np.all(c[~eq] <= nlp.g_U[~eq] + tol))
+
+
+def _check(g, h, k, n_states, inst):
+    """Same status.  Solves that never left the original problem agree on the states
+    within 1e-6 and on every variable (lambda included) within 1e-4.  A solve that
+    went through IPOPT's restoration phase follows a path on which last-bit
+    differences (device libm vs glibc) are amplified, so the two builds may land on
+    different local minima of this nonconvex NLP: both must then be feasible solutions."""
     assert g.status[k] == h.status[k]
-    if g.status[k] in (0, 1):
+    if g.status[k] not in (0, 1):
+        return
+    if g.n_resto[k] == 0 and h.n_resto[k] == 0:
         assert np.max(np.abs(g.x[k][:n_states] - h.x[k][:n_states])) < 1e-6
         assert np.max(np.abs(g.x[k] - h.x[k])) < 1e-4
+    else:
+        assert _feasible(inst, g.x[k]) and _feasible(inst, h.x[k])
 
 
 def test_gpu_matches_host_core_quads(ctx):
@@ -37,8 +50,8 @@ def test_gpu_matches_host_core_quads(ctx):
     g = ctx.solve_points(_native.PointsPackedBatch(insts))
     h = H.solve_points(insts)
     for k in range(len(insts)):
-        _check(g, h, k, 5 * 12)
-    assert np.mean(g.status == 0) >= 0.85
+        _check(g, h, k, 5 * 12, insts[k])
+    assert np.mean(np.isin(g.status, (0, 1))) >= 0.98     # restoration recovers the former line-search failures
 
 
 def test_gpu_matches_oracle_mower_and_mixed_edges(ctx):
@@ -57,7 +70,7 @@ def test_gpu_matches_oracle_mower_and_mixed_edges(ctx):
     g = ctx.solve_points(_native.PointsPackedBatch(b))   # EM = 8 kernel (padded edges)
     h = H.solve_points(b)
     for k in range(2):
-        _check(g, h, k, 5 * 10)
+        _check(g, h, k, 5 * 10, b[k])
 
 
 def test_gpu_config_b_shape_properties(ctx):
@@ -73,7 +86,7 @@ def test_gpu_config_b_shape_properties(ctx):
         eq = nlp.g_L == nlp.g_U
         assert np.max(np.abs(c[eq] - nlp.g_L[eq])) < 1e-6
         assert np.all(c[~eq] >= nlp.g_L[~eq] - 1e-6) and np.all(c[~eq] <= nlp.g_U[~eq] + 1e-6)
-    assert np.mean(np.isin(g.status, (0, 1))) >= 0.75
+    assert np.mean(np.isin(g.status, (0, 1))) >= 0.98
 
 
 def test_shim_end_to_end(ctx):
