@@ -24,6 +24,7 @@ struct ThreadWave {
   template <class T>
   using cst = const T;
   static constexpr int width = 64;
+  static constexpr bool kMfma = false;
   int lane;
   double* lds;
   int* ildsp;

@@ -2168,6 +2168,121 @@ struct ObcaSolver {
     return bad;
   }
 
+#if defined(__HIPCC__)
+  // ------------------------------------------------ Riccati factor on the matrix core
+  // Same recursion as riccati_factor, written as 16x16 fp64 MFMA tiles over the
+  // augmented stage variables [z_i (nz) ; v_i (nv)] (nz = 5 + nv, nz + nv <= 11):
+  //   M = H_i + F_i' P_{i+1} F_i,   F_i = [[Jx, 0, Jv], [0, 0, I]]  (z_{i+1} = F_i [z_i; v_i])
+  //   Rt = M_vv, St = M_vz, K = -Rt^-1 St, P_i = M_zz + St' K.
+  // Layout (v_mfma_f64_16x16x4f64): lane l holds column l&15 and rows (l>>4) + 4r in register r.
+  // A symmetric P in that layout is directly the A operand (k-step s = register s), F's rows
+  // are both the B operand of P F and the A operand of F' (P F), and the accumulator of P F
+  // is the B operand of F' (P F): 5 MFMAs per stage, no lane shuffles; Rt / St go through LDS.
+  HTP_HD HTP_FI int riccati_factor_mfma() {
+    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
+    const int64_t nb2 = (int64_t)nb * nb;
+    const int col = c.lane & 15, rg = c.lane >> 4;
+    ld* Mv = c.lds;           // 3 x 16: rows v of M
+    ld* Pb = c.lds + 48;      // 8 x 8: P_i before symmetrisation
+    // stage-independent gather maps of this lane: H in the C layout (4 registers), F rows (2 registers)
+    // source codes: 0 zero, 1 Kst w-block (offset), 2 Off jerk cross (offset), 3 J (offset), 4 one
+    int hk[4], ho[4], fk[2], fo[2];
+    auto widx = [&](int a) { return a < NS ? a : (a >= nz && a < nz + nv ? NS + (a - nz) : -1); };
+    for (int r = 0; r < 4; ++r) {
+      const int row = rg + 4 * r, wr = widx(row), wc = widx(col);
+      hk[r] = 0; ho[r] = 0;
+      if (wr >= 0 && wc >= 0) { hk[r] = 1; ho[r] = (NS + wr) * nb + NS + wc; }
+      else if (row >= nz && row - nz < 2 && col >= NS && col < nz) { hk[r] = 2; ho[r] = (NS + 5 + row - nz) * nb + NS + 5 + (col - NS); }
+      else if (col >= nz && col - nz < 2 && row >= NS && row < nz) { hk[r] = 2; ho[r] = (NS + 5 + col - nz) * nb + NS + 5 + (row - NS); }
+    }
+    for (int sgm = 0; sgm < 2; ++sgm) {
+      const int row = rg + 4 * sgm;
+      fk[sgm] = 0; fo[sgm] = 0;
+      if (row < NS) {
+        if (col < NS) { fk[sgm] = 3; fo[sgm] = JOFF + row * 8 + col; }
+        else if (col >= nz && col < nz + nv) { fk[sgm] = 3; fo[sgm] = JOFF + row * 8 + NS + (col - nz); }
+      } else if (row < nz && col == nz + (row - NS)) {
+        fk[sgm] = 4;
+      }
+    }
+    const gd* Kst = A(L.Kst);
+    const gd* Off = A(L.Off);
+    const gd* LDa = A(L.LD);
+    auto ld_h = [&](int i, double* h) {
+      for (int r = 0; r < 4; ++r) {
+        double v = 0.0;
+        if (hk[r] == 1) v = Kst[(int64_t)i * nb2 + ho[r]];
+        else if (hk[r] == 2 && i >= 1) v = Off[(int64_t)i * nb2 + ho[r]];
+        h[r] = v;
+      }
+    };
+    auto ld_f = [&](int i, double* f) {
+      for (int sgm = 0; sgm < 2; ++sgm) f[sgm] = fk[sgm] == 3 ? LDa[(int64_t)i * nb2 + fo[sgm]] : (fk[sgm] == 4 ? 1.0 : 0.0);
+    };
+    // P_{N-1} = [[H_xx, 0], [0, 0]]
+    dbl4 Pc;
+    {
+      gd* Ps = A(L.LD) + (int64_t)(N - 1) * nb2;
+      for (int r = 0; r < 4; ++r) {
+        const int row = rg + 4 * r;
+        const double v = (row < NS && col < NS) ? Kst[(int64_t)(N - 1) * nb2 + (NS + row) * nb + NS + col] : 0.0;
+        Pc[r] = v;
+        if (row < 8 && col < 8) Ps[row * 8 + col] = v;
+      }
+    }
+    int bad = 0;
+    double hcur[4], fcur[2], hnxt[4], fnxt[2];
+    if (N >= 2) { ld_h(N - 2, hcur); ld_f(N - 2, fcur); }
+    for (int i = N - 2; i >= 0; --i) {
+      HTP_PROF0();
+      if (i > 0) { ld_h(i - 1, hnxt); ld_f(i - 1, fnxt); }  // next stage's record, in flight during this one
+      dbl4 Y = {0.0, 0.0, 0.0, 0.0};
+      Y = Ctx::mfma16(Pc[0], fcur[0], Y);
+      Y = Ctx::mfma16(Pc[1], fcur[1], Y);
+      dbl4 M = {hcur[0], hcur[1], hcur[2], hcur[3]};
+      M = Ctx::mfma16(fcur[0], Y[0], M);
+      M = Ctx::mfma16(fcur[1], Y[1], M);
+      for (int r = 0; r < 4; ++r) {
+        const int row = rg + 4 * r;
+        if (row >= nz && row < nz + nv) Mv[(row - nz) * 16 + col] = M[r];
+      }
+      c.sync();
+      HTP_PROF(1);
+      double Rl[9], Lc[9];
+      for (int k = 0; k < 9; ++k) Rl[k] = (k / 3 < nv && k % 3 < nv) ? Mv[(k / 3) * 16 + nz + k % 3] : 0.0;
+      const bool pd = chol3(Rl, nv, Lc);
+      if (!pd) ++bad;
+      double stc[3] = {0.0, 0.0, 0.0};
+      for (int a = 0; a < 3; ++a)
+        if (a < nv && col < nz) stc[a] = Mv[a * 16 + col];
+      const double stA = (rg < nv && col < nz) ? stc[rg] : 0.0;  // St' as the A operand: St[rg][col]
+      if (pd) chol3_solve(Lc, nv, stc);
+      const double kB = (rg < nv && col < nz) ? -stc[rg] : 0.0;  // K[rg][col] as the B operand
+      HTP_PROF(3);
+      const dbl4 Pn = Ctx::mfma16(stA, kB, M);
+      gd* Ps = A(L.LD) + (int64_t)i * nb2;
+      for (int r = 0; r < 2; ++r) {
+        const int row = rg + 4 * r;
+        const double v = (row < nz && col < nz) ? Pn[r] : 0.0;
+        if (col < 8) { Pb[row * 8 + col] = v; Ps[row * 8 + col] = v; }
+      }
+      if (rg < 3 && col < 8) Ps[64 + rg * 8 + col] = (rg < nv && col < nz) ? kB : 0.0;
+      if (c.lane < 9) Ps[88 + c.lane] = Lc[c.lane];
+      c.sync();
+      for (int r = 0; r < 4; ++r) {  // P_i = (Pn + Pn') / 2, zero outside nz x nz
+        const int row = rg + 4 * r;
+        Pc[r] = (r < 2 && row < nz && col < nz) ? 0.5 * (Pb[row * 8 + col] + Pb[col * 8 + row]) : 0.0;
+      }
+      c.sync();
+      for (int r = 0; r < 4; ++r) hcur[r] = hnxt[r];
+      fcur[0] = fnxt[0];
+      fcur[1] = fnxt[1];
+      HTP_PROF(5);
+    }
+    return bad;
+  }
+#endif
+
   // V (block order [y|x|u|tau]) -> X (same order) with the Riccati factor.
   // Each stage's inputs are packed into a fixed 128/192-entry record that the
   // wave loads with one coalesced round trip, one stage ahead of use
@@ -2426,7 +2541,12 @@ struct ObcaSolver {
     cyc[1] += t2 - t1;
     // (the point formulation's hard terminal rows have no Riccati form: block LDL^T)
     if (!PT && dc == 0.0 && !rs) {
-      const int bad = riccati_factor();
+      int bad;
+#if defined(__HIPCC__)
+      if constexpr (Ctx::kMfma) bad = riccati_factor_mfma();
+      else
+#endif
+        bad = riccati_factor();
       use_ric = true;
       cyc[2] += c.clock() - t2;
       neg_out = bad ? -1 : neg + NS * N + NS + D.md;

@@ -8,6 +8,8 @@
 namespace htp {
 
 #if defined(__HIPCC__)
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
 struct DevWave {
   using gd = __attribute__((address_space(1))) double;  // HBM (global) doubles
   using ld = __attribute__((address_space(3))) double;  // LDS doubles
@@ -15,6 +17,7 @@ struct DevWave {
   template <class T>
   using cst = const __attribute__((address_space(4))) T;  // constant (scalar-cached) memory
   static constexpr int width = 64;
+  static constexpr bool kMfma = true;  // v_mfma_f64_16x16x4f64 available (gfx950)
   int lane;
   ld* lds;    // per-wave LDS scratch
   li* ildsp;  // per-wave LDS int scratch
@@ -60,6 +63,11 @@ struct DevWave {
   __device__ __forceinline__ long long clock() const { return (long long)__builtin_amdgcn_s_memtime(); }
   // constant-rate wall clock (hipDeviceAttributeWallClockRate ticks/s), for max_cpu_time
   __device__ __forceinline__ long long wall() const { return (long long)wall_clock64(); }
+  // D = A (16x4) B (4x16) + C in fp64 on the matrix core.  Lane l supplies a = A[l&15][l>>4] and
+  // b = B[l>>4][l&15]; c/d[r] = C[(l>>4) + 4r][l&15] (MI355X_MICROARCH / cdna_hip_programming f64 map).
+  __device__ __forceinline__ static dbl4 mfma16(double a, double b, dbl4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  }
 };
 #endif
 
@@ -70,6 +78,7 @@ struct HostLane {
   template <class T>
   using cst = const T;
   static constexpr int width = 1;
+  static constexpr bool kMfma = false;
   int lane = 0;
   double* lds;
   int* ildsp;
