@@ -2169,15 +2169,35 @@ struct ObcaSolver {
   }
 
 #if defined(__HIPCC__)
-  // ------------------------------------------------ Riccati factor on the matrix core
-  // Same recursion as riccati_factor, written as 16x16 fp64 MFMA tiles over the
-  // augmented stage variables [z_i (nz) ; v_i (nv)] (nz = 5 + nv, nz + nv <= 11):
-  //   M = H_i + F_i' P_{i+1} F_i,   F_i = [[Jx, 0, Jv], [0, 0, I]]  (z_{i+1} = F_i [z_i; v_i])
-  //   Rt = M_vv, St = M_vz, K = -Rt^-1 St, P_i = M_zz + St' K.
-  // Layout (v_mfma_f64_16x16x4f64): lane l holds column l&15 and rows (l>>4) + 4r in register r.
-  // A symmetric P in that layout is directly the A operand (k-step s = register s), F's rows
-  // are both the B operand of P F and the A operand of F' (P F), and the accumulator of P F
-  // is the B operand of F' (P F): 5 MFMAs per stage, no lane shuffles; Rt / St go through LDS.
+  // ------------------------------------------------ Riccati recursion on the matrix core
+  // Same recursion as riccati_factor / riccati_solve, written as 16x16 fp64 MFMA tiles over the
+  // augmented stage variables u_i = [z_i (rows 0..7, z = [x, u_{i-1}, tau_{i-1}] zero-padded to 8) ;
+  // v_i (rows 8..8+nv)], with z_{i+1} = F_i u_i + e_{i+1},  F_i = [[Jx, 0, Jv], [0, 0, I]]:
+  //   factor:  M = H_i + F_i' P_{i+1} F_i,  Rt = M_vv, St = M_vz, K = -Rt^-1 St, P_i = M_zz + St' K
+  //   backward: w = p_{i+1} - P_{i+1} e_{i+1}, g = [q_i; r_i] + F_i' w, rt_i = g_v, p_i = g_z + K_i' rt_i
+  //   forward:  y_i = p_i - P_i z_i, u_i = [z_i; Rt^-1 rt_i + K_i z_i], z_{i+1} = F_i u_i + e_{i+1}
+  // Layout (v_mfma_f64_16x16x4f64): lane l holds column l&15 and rows (l>>4) + 4r in register r;
+  // vectors live in column 0.  A symmetric P in that layout is the A operand of P F (k-step s =
+  // register s); F's rows (FR) are the B operand of P F and the A operand of F' (.); every product's
+  // accumulator is the B operand of the next one, so no lane shuffles are needed; Rt / St of the
+  // factor go through LDS.  5 MFMAs per stage in the factor and in each solve pass.
+  static constexpr int V0 = 8;  // row of v_i in u_i
+  // F_i[frow][fcol] (fcol over u_i): stage-independent source of this lane's element
+  struct FSrc { int kind, off; };  // 0 zero, 3 J (offset in the LD slot), 4 one
+  HTP_HD HTP_FI FSrc f_src(int frow, int fcol) const {
+    const int nv = D.nw - NS;
+    if (frow < NS) {
+      if (fcol < NS) return FSrc{3, JOFF + frow * 8 + fcol};
+      if (fcol >= V0 && fcol < V0 + nv) return FSrc{3, JOFF + frow * 8 + NS + (fcol - V0)};
+      return FSrc{0, 0};
+    }
+    if (frow < NS + nv && fcol == V0 + (frow - NS)) return FSrc{4, 0};
+    return FSrc{0, 0};
+  }
+  HTP_HD HTP_FI double f_get(const FSrc& f, const gd* slot) const {
+    return f.kind == 3 ? slot[f.off] : (f.kind == 4 ? 1.0 : 0.0);
+  }
+
   HTP_HD HTP_FI int riccati_factor_mfma() {
     const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
     const int64_t nb2 = (int64_t)nb * nb;
@@ -2185,26 +2205,18 @@ struct ObcaSolver {
     ld* Mv = c.lds;           // 3 x 16: rows v of M
     ld* Pb = c.lds + 48;      // 8 x 8: P_i before symmetrisation
     // stage-independent gather maps of this lane: H in the C layout (4 registers), F rows (2 registers)
-    // source codes: 0 zero, 1 Kst w-block (offset), 2 Off jerk cross (offset), 3 J (offset), 4 one
-    int hk[4], ho[4], fk[2], fo[2];
-    auto widx = [&](int a) { return a < NS ? a : (a >= nz && a < nz + nv ? NS + (a - nz) : -1); };
+    // H sources: 0 zero, 1 Kst w-block (offset), 2 Off jerk cross (offset)
+    int hk[4], ho[4];
+    FSrc fs[2];
+    auto widx = [&](int a) { return a < NS ? a : (a >= V0 && a < V0 + nv ? NS + (a - V0) : -1); };
     for (int r = 0; r < 4; ++r) {
       const int row = rg + 4 * r, wr = widx(row), wc = widx(col);
       hk[r] = 0; ho[r] = 0;
       if (wr >= 0 && wc >= 0) { hk[r] = 1; ho[r] = (NS + wr) * nb + NS + wc; }
-      else if (row >= nz && row - nz < 2 && col >= NS && col < nz) { hk[r] = 2; ho[r] = (NS + 5 + row - nz) * nb + NS + 5 + (col - NS); }
-      else if (col >= nz && col - nz < 2 && row >= NS && row < nz) { hk[r] = 2; ho[r] = (NS + 5 + col - nz) * nb + NS + 5 + (row - NS); }
+      else if (row >= V0 && row - V0 < 2 && col >= NS && col < nz) { hk[r] = 2; ho[r] = (NS + 5 + row - V0) * nb + NS + 5 + (col - NS); }
+      else if (col >= V0 && col - V0 < 2 && row >= NS && row < nz) { hk[r] = 2; ho[r] = (NS + 5 + col - V0) * nb + NS + 5 + (row - NS); }
     }
-    for (int sgm = 0; sgm < 2; ++sgm) {
-      const int row = rg + 4 * sgm;
-      fk[sgm] = 0; fo[sgm] = 0;
-      if (row < NS) {
-        if (col < NS) { fk[sgm] = 3; fo[sgm] = JOFF + row * 8 + col; }
-        else if (col >= nz && col < nz + nv) { fk[sgm] = 3; fo[sgm] = JOFF + row * 8 + NS + (col - nz); }
-      } else if (row < nz && col == nz + (row - NS)) {
-        fk[sgm] = 4;
-      }
-    }
+    for (int sgm = 0; sgm < 2; ++sgm) fs[sgm] = f_src(rg + 4 * sgm, col);
     const gd* Kst = A(L.Kst);
     const gd* Off = A(L.Off);
     const gd* LDa = A(L.LD);
@@ -2217,7 +2229,7 @@ struct ObcaSolver {
       }
     };
     auto ld_f = [&](int i, double* f) {
-      for (int sgm = 0; sgm < 2; ++sgm) f[sgm] = fk[sgm] == 3 ? LDa[(int64_t)i * nb2 + fo[sgm]] : (fk[sgm] == 4 ? 1.0 : 0.0);
+      for (int sgm = 0; sgm < 2; ++sgm) f[sgm] = f_get(fs[sgm], LDa + (int64_t)i * nb2);
     };
     // P_{N-1} = [[H_xx, 0], [0, 0]]
     dbl4 Pc;
@@ -2242,14 +2254,11 @@ struct ObcaSolver {
       dbl4 M = {hcur[0], hcur[1], hcur[2], hcur[3]};
       M = Ctx::mfma16(fcur[0], Y[0], M);
       M = Ctx::mfma16(fcur[1], Y[1], M);
-      for (int r = 0; r < 4; ++r) {
-        const int row = rg + 4 * r;
-        if (row >= nz && row < nz + nv) Mv[(row - nz) * 16 + col] = M[r];
-      }
+      if (rg < nv) Mv[rg * 16 + col] = M[2];  // rows V0 + rg (register 2)
       c.sync();
       HTP_PROF(1);
       double Rl[9], Lc[9];
-      for (int k = 0; k < 9; ++k) Rl[k] = (k / 3 < nv && k % 3 < nv) ? Mv[(k / 3) * 16 + nz + k % 3] : 0.0;
+      for (int k = 0; k < 9; ++k) Rl[k] = (k / 3 < nv && k % 3 < nv) ? Mv[(k / 3) * 16 + V0 + k % 3] : 0.0;
       const bool pd = chol3(Rl, nv, Lc);
       if (!pd) ++bad;
       double stc[3] = {0.0, 0.0, 0.0};
@@ -2281,7 +2290,140 @@ struct ObcaSolver {
     }
     return bad;
   }
+
+  // V (block order [y|x|u|tau]) -> X (same order), the two passes on the matrix core
+  HTP_HD HTP_FI void riccati_solve_mfma(const gd* V, gd* X) {
+    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
+    const int64_t nb2 = (int64_t)nb * nb;
+    const int col = c.lane & 15, rg = c.lane >> 4;
+    const bool c0 = col == 0;
+    const gd* LDa = A(L.LD);
+    // per-lane record maps: F rows as B / F' as A (2), F as A (3), P as A (2), K' as A (1), K at rows V0.. as A (2)
+    FSrc fT[2], fA[3];
+    for (int sgm = 0; sgm < 2; ++sgm) fT[sgm] = f_src(rg + 4 * sgm, col);
+    for (int sgm = 0; sgm < 3; ++sgm) fA[sgm] = f_src(col, rg + 4 * sgm);
+    auto p_at = [&](const gd* slot, int sgm) {  // P[col][4 sgm + rg] (P symmetric, 8 x 8 stride 8)
+      const int k = rg + 4 * sgm;
+      return (col < nz && k < nz) ? slot[col * 8 + k] : 0.0;
+    };
+    // ---------------- backward
+    // p_{N-1} = [q_{N-1}; 0]
+    dbl4 pv = {0.0, 0.0, 0.0, 0.0};
+    for (int r = 0; r < 2; ++r) {
+      const int row = rg + 4 * r;
+      pv[r] = (c0 && row < NS) ? V[(int64_t)(N - 1) * nb + NS + row] : 0.0;
+    }
+    {
+      gd* Xl = X + (int64_t)(N - 1) * nb;
+      for (int r = 0; r < 2; ++r) {
+        const int row = rg + 4 * r;
+        if (c0 && row < 8) Xl[row] = pv[r];
+      }
+    }
+    // stage-i record of the backward pass: -P_{i+1} (A, 2), F_i' (A, 2), K_i' (A, 1), [q_i; r_i] (C, 3),
+    // e_{i+1} (B, 2, unscaled)
+    struct BRec { double mp[2], ft[2], kt, qr[3], e[2]; };
+    auto ld_b = [&](int i, BRec& R) {
+      const gd* slot = LDa + (int64_t)i * nb2;
+      const gd* nslot = slot + nb2;
+      for (int sgm = 0; sgm < 2; ++sgm) {
+        R.mp[sgm] = -p_at(nslot, sgm);
+        R.ft[sgm] = f_get(fT[sgm], slot);
+        const int row = rg + 4 * sgm;
+        R.e[sgm] = (c0 && row < NS) ? V[(int64_t)(i + 1) * nb + row] * nslot[SOFF + row] : 0.0;
+      }
+      R.kt = (rg < nv && col < nz) ? slot[64 + rg * 8 + col] : 0.0;
+      for (int r = 0; r < 3; ++r) {
+        const int row = rg + 4 * r;
+        double v = 0.0;
+        if (c0 && row < NS) v = V[(int64_t)i * nb + NS + row];
+        else if (c0 && row >= V0 && row < V0 + nv) v = V[(int64_t)i * nb + NS + NS + (row - V0)];
+        R.qr[r] = v;
+      }
+    };
+    BRec bc, bn;
+    if (N >= 2) ld_b(N - 2, bc);
+    for (int i = N - 2; i >= 0; --i) {
+      if (i > 0) ld_b(i - 1, bn);
+      dbl4 w = Ctx::mfma16(bc.mp[0], bc.e[0], pv);          // w = p - P e
+      w = Ctx::mfma16(bc.mp[1], bc.e[1], w);
+      dbl4 g = {bc.qr[0], bc.qr[1], bc.qr[2], 0.0};         // g = [q; r] + F' w
+      g = Ctx::mfma16(bc.ft[0], w[0], g);
+      g = Ctx::mfma16(bc.ft[1], w[1], g);
+      pv = Ctx::mfma16(bc.kt, g[2], g);                      // p = g_z + K' rt   (rt = g rows V0..)
+      gd* Xi = X + (int64_t)i * nb;
+      for (int r = 0; r < 2; ++r) {
+        const int row = rg + 4 * r;
+        if (c0 && row < nz) Xi[row] = pv[r];
+      }
+      if (c0 && rg < nv) Xi[nz + rg] = g[2];
+      bc = bn;
+    }
+    c.sync();
+    HTP_PROF(6);
+    // ---------------- forward: z_0 = [V_0[0:5] / sc; 0]
+    const gd* scE = A(L.scE);
+    dbl4 zu = {0.0, 0.0, 0.0, 0.0};  // [z_i; v_i] in column 0
+    for (int r = 0; r < 2; ++r) {
+      const int row = rg + 4 * r;
+      zu[r] = (c0 && row < NS) ? V[row] / scE[row] : 0.0;
+    }
+    // stage-i record of the forward pass: -P_i (A, 2), p_i (C, 2), K_i at rows V0.. (A, 2), F_i (A, 3),
+    // e_{i+1} (C, 2), rt_i (3) + chol(Rt_i) (9), 1/sc of y_i (2)
+    struct FRec { double mp[2], p[2], ka[2], fa[3], e[2], rt[3], lc[9], isc[2]; };
+    auto ld_f = [&](int i, FRec& R) {
+      const gd* slot = LDa + (int64_t)i * nb2;
+      const gd* Xi = X + (int64_t)i * nb;
+      const bool last = i >= N - 1;
+      for (int sgm = 0; sgm < 2; ++sgm) {
+        const int row = rg + 4 * sgm, k = rg + 4 * sgm;
+        R.mp[sgm] = -p_at(slot, sgm);
+        R.p[sgm] = (c0 && row < nz) ? Xi[row] : 0.0;
+        R.ka[sgm] = (!last && col >= V0 && col < V0 + nv && k < nz) ? slot[64 + (col - V0) * 8 + k] : 0.0;
+        R.e[sgm] = (!last && c0 && row < NS) ? V[(int64_t)(i + 1) * nb + row] * slot[nb2 + SOFF + row] : 0.0;
+        R.isc[sgm] = (row < NS) ? slot[SOFF + row] : 0.0;
+      }
+      for (int sgm = 0; sgm < 3; ++sgm) R.fa[sgm] = last ? 0.0 : f_get(fA[sgm], slot);
+      for (int a = 0; a < 3; ++a) R.rt[a] = (!last && a < nv) ? Xi[nz + a] : 0.0;
+      for (int k = 0; k < 9; ++k) R.lc[k] = last ? 0.0 : slot[88 + k];
+    };
+    FRec fc, fn;
+    ld_f(0, fc);
+    for (int i = 0; i < N; ++i) {
+      if (i + 1 < N) ld_f(i + 1, fn);
+      dbl4 y = {fc.p[0], fc.p[1], 0.0, 0.0};                 // y = p - P z
+      y = Ctx::mfma16(fc.mp[0], zu[0], y);
+      y = Ctx::mfma16(fc.mp[1], zu[1], y);
+      gd* Xi = X + (int64_t)i * nb;
+      const double zr0 = zu[0], zr1 = zu[1];
+      for (int r = 0; r < 2; ++r) {
+        const int row = rg + 4 * r;
+        if (c0 && row < NS) Xi[row] = y[r] * fc.isc[r];
+      }
+      if (i < N - 1) {
+        double kv[3] = {fc.rt[0], fc.rt[1], fc.rt[2]};
+        chol3_solve(fc.lc, nv, kv);
+        dbl4 u = {zu[0], zu[1], (c0 && rg < nv) ? kv[rg] : 0.0, 0.0};  // u = [z; Rt^-1 rt + K z]
+        u = Ctx::mfma16(fc.ka[0], zu[0], u);
+        u = Ctx::mfma16(fc.ka[1], zu[1], u);
+        if (c0 && rg < nv) Xi[NS + NS + rg] = u[2];
+        dbl4 zn = {fc.e[0], fc.e[1], 0.0, 0.0};              // z_{i+1} = F u + e
+        zn = Ctx::mfma16(fc.fa[0], u[0], zn);
+        zn = Ctx::mfma16(fc.fa[1], u[1], zn);
+        zn = Ctx::mfma16(fc.fa[2], u[2], zn);
+        zu = zn;
+      }
+      for (int r = 0; r < 2; ++r) {
+        const int row = rg + 4 * r;
+        if (c0 && row < NS) Xi[NS + row] = r == 0 ? zr0 : zr1;
+      }
+      fc = fn;
+    }
+    c.sync();
+    HTP_PROF(7);
+  }
 #endif
+
 
   // V (block order [y|x|u|tau]) -> X (same order) with the Riccati factor.
   // Each stage's inputs are packed into a fixed 128/192-entry record that the
@@ -2682,7 +2824,11 @@ struct ObcaSolver {
     c.sync();
     gd* X = A(L.X);
     if (use_ric) {
-      riccati_solve(V, X);
+#if defined(__HIPCC__)
+      if constexpr (Ctx::kMfma) riccati_solve_mfma(V, X);
+      else
+#endif
+        riccati_solve(V, X);
     } else {
     // forward: V_i -= LD_i V_{i-1}
     for (int i = 1; i < D.nblk; ++i) {
