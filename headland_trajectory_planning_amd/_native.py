@@ -87,7 +87,9 @@ EXPORTS = ["htp_obca_sizes", "htp_create", "htp_destroy", "htp_last_error", "htp
            "htp_hastar_search_batch", "htp_hastar_search_batch_device", "htp_hastar_last_ms",
            "htp_ypark_search_batch", "htp_ypark_search_batch_device", "htp_ypark_last_ms",
            "htp_obca_points_sizes", "htp_obca_points_solve_batch", "htp_obca_points_solve_batch_device",
-           "htp_init_ref_path_batch", "htp_init_ref_path_batch_device", "htp_init_ref_path_last_ms"]
+           "htp_init_ref_path_batch", "htp_init_ref_path_batch_device", "htp_init_ref_path_last_ms",
+           "htp_queue_create", "htp_queue_destroy", "htp_queue_publish", "htp_queue_close", "htp_queue_published",
+           "htp_queue_claimed", "htp_obca_solve_queue_device", "htp_obca_resident_waves"]
 
 
 def _declare(lib):
@@ -146,6 +148,24 @@ def _declare(lib):
     lib.htp_ypark_search_batch_device.restype = ctypes.c_int
     lib.htp_ypark_last_ms.argtypes = [ctypes.c_void_p]
     lib.htp_ypark_last_ms.restype = ctypes.c_double
+    lib.htp_queue_create.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    lib.htp_queue_create.restype = ctypes.c_void_p
+    lib.htp_queue_destroy.argtypes = [ctypes.c_void_p]
+    lib.htp_queue_destroy.restype = None
+    lib.htp_queue_publish.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+    lib.htp_queue_publish.restype = ctypes.c_int
+    lib.htp_queue_close.argtypes = [ctypes.c_void_p]
+    lib.htp_queue_close.restype = ctypes.c_int
+    lib.htp_queue_published.argtypes = [ctypes.c_void_p]
+    lib.htp_queue_published.restype = ctypes.c_int64
+    lib.htp_queue_claimed.argtypes = [ctypes.c_void_p]
+    lib.htp_queue_claimed.restype = ctypes.c_int64
+    lib.htp_obca_solve_queue_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ObcaBatch), ctypes.c_void_p,
+                                                ctypes.POINTER(ObcaResult), ctypes.c_void_p, ctypes.c_int32,
+                                                ctypes.c_double]
+    lib.htp_obca_solve_queue_device.restype = ctypes.c_int
+    lib.htp_obca_resident_waves.argtypes = [ctypes.c_void_p, ctypes.POINTER(ObcaBatch)]
+    lib.htp_obca_resident_waves.restype = ctypes.c_int32
     return lib
 
 
@@ -270,6 +290,30 @@ class PackedBatch:
         for name in ("traj", "obs_A", "obs_b", "body_G", "body_g", "params", "init_control", "init_mu", "init_lambda"):
             setattr(b, name, src[name] if name in src else ptr(getattr(self, name)))
         return b
+
+    INPUTS = ("traj", "obs_A", "obs_b", "body_G", "body_g", "params", "init_control", "init_mu", "init_lambda")
+
+    def chunk_struct(self, ptrs, lo, hi):
+        """htp_obca_batch of problems [lo, hi) over base pointers `ptrs` (device or
+        host) laid out like this batch's arrays (problem-major)."""
+        b = self.struct(ptrs)
+        b.batch = int(hi - lo)
+        for name in self.INPUTS:
+            a = getattr(self, name)
+            base = ptrs[name] if name in ptrs else (None if a is None else a.ctypes.data)
+            setattr(b, name, None if base is None else base + int(lo) * a.strides[0])
+        return b
+
+    @classmethod
+    def concat(cls, parts):
+        """One batch from same-shape PackedBatches (problem order kept)."""
+        out = cls.__new__(cls)
+        out.__dict__.update(parts[0].__dict__)
+        out.batch = sum(p.batch for p in parts)
+        for name in cls.INPUTS:
+            a = [getattr(p, name) for p in parts]
+            setattr(out, name, None if a[0] is None else np.ascontiguousarray(np.concatenate(a, axis=0)))
+        return out
 
 
 class ObcaPointsBatch(ctypes.Structure):  # htp_obca_points_batch
@@ -585,6 +629,42 @@ class YparkResults:
         return r
 
 
+class WorkQueue:
+    """Host work queue of problem indices feeding one persistent solve launch
+    (htp_queue_*: pinned, GPU-coherent host memory)."""
+
+    def __init__(self, ctx, capacity):
+        self.lib = ctx.lib
+        self.q = self.lib.htp_queue_create(ctx.ctx, int(capacity))
+        if not self.q:
+            raise RuntimeError(f"[htp] htp_queue_create failed: {ctx.error()}")
+
+    def publish(self, pids):
+        a = np.ascontiguousarray(np.asarray(pids, dtype=np.int32))
+        if self.lib.htp_queue_publish(self.q, a.ctypes.data, a.size) != 0:
+            raise RuntimeError("[htp] htp_queue_publish failed (full, closed or index out of range)")
+
+    def close(self):
+        self.lib.htp_queue_close(self.q)
+
+    def published(self):
+        return int(self.lib.htp_queue_published(self.q))
+
+    def claimed(self):
+        return int(self.lib.htp_queue_claimed(self.q))
+
+    def destroy(self):
+        if self.q:
+            self.lib.htp_queue_destroy(self.q)
+            self.q = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
 class Context:
     """Owns one htp_ctx (device workspace)."""
 
@@ -631,8 +711,9 @@ class Context:
     def init_ref_path_last_ms(self):
         return self.lib.htp_init_ref_path_last_ms(self.ctx)
 
-    def solve_device(self, packed, dev_ptrs, out_ptrs, stream=None):
-        b = packed.struct(dev_ptrs)
+    def solve_device(self, packed, dev_ptrs, out_ptrs, stream=None, lo=None, hi=None):
+        """Device-resident solve of `packed` (or of its problems [lo, hi)) on `stream`."""
+        b = packed.struct(dev_ptrs) if lo is None else packed.chunk_struct(dev_ptrs, lo, hi)
         r = ObcaResult()
         for k, v in out_ptrs.items():
             setattr(r, k, v)
@@ -642,6 +723,23 @@ class Context:
 
     def last_kernel_ms(self):
         return self.lib.htp_last_kernel_ms(self.ctx)
+
+    def resident_waves(self, packed):
+        v = self.lib.htp_obca_resident_waves(self.ctx, ctypes.byref(packed.struct()))
+        if v <= 0:
+            raise RuntimeError(f"[htp] htp_obca_resident_waves failed: {self.error()}")
+        return v
+
+    def solve_queue_device(self, packed, dev_ptrs, queue, out_ptrs, stream=None, waves=0, max_wait_s=60.0):
+        """Persistent launch over the resident problems of `packed`, fed by `queue` (WorkQueue)."""
+        b = packed.struct(dev_ptrs)
+        r = ObcaResult()
+        for k, v in out_ptrs.items():
+            setattr(r, k, v)
+        rc = self.lib.htp_obca_solve_queue_device(self.ctx, ctypes.byref(b), queue.q, ctypes.byref(r), stream,
+                                                  int(waves), float(max_wait_s))
+        if rc != 0:
+            raise RuntimeError(f"[htp] htp_obca_solve_queue_device failed: {self.error()}")
 
     def last_cycles(self, batch):
         """[batch, 8] shader-cycle counters: local sweeps, stage assembly,

@@ -23,7 +23,6 @@ extern "C" int htp_cpu_obca_solve_range(const htp_obca_batch* in, htp_obca_resul
   if (check_shape(in, &e) || first < 0 || first + count > in->batch) return -1;
   Options o = default_options();
   o.wall_rate = 1e9;
-  o.wall_rate = 1e9;
   Dims D;
   make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
   const Layout L = make_layout(D);

@@ -14,6 +14,7 @@ struct htp_ctx {
   Options opt = htp::default_options();
   double wall_rate = 1e8;   // device wall-clock ticks/s (hipDeviceAttributeWallClockRate)
   void* ws = nullptr;
+  void* next = nullptr;     // device ticket counter of the solve launch
   size_t ws_bytes = 0;
   void* scratch = nullptr;  // Result array
   size_t scratch_bytes = 0;

@@ -8,6 +8,8 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <cstdint>
 #include <string>
 #include <vector>
 
@@ -36,29 +38,98 @@ inline unsigned lds_pad_bytes() {
   return (unsigned)(want > 160 * 1024 ? 160 * 1024 - fixed : want - fixed);
 }
 
+// Work source of a solve launch: a static range (ticket t solves problem t, t <
+// n_static) or a host work queue (htp_queue_*: ticket t solves items[t] once the
+// host has published it).
+struct QueueHost {              // pinned, GPU-coherent host memory
+  long long avail;              // tickets published (host writes, release)
+  int closed;                   // no more tickets will be published
+  int pad0;
+  long long pad1[6];
+  long long claimed;            // claim hint written by the waves (separate line)
+  long long pad2[7];
+  int items[1];                 // [capacity] problem indices
+};
+struct WorkSrc {
+  unsigned long long* next;     // device ticket counter (agent-scope atomics)
+  QueueHost* q;                 // nullptr: static range
+  long long n_static;
+  long long max_wait;           // device wall-clock ticks a wave may wait for a ticket
+};
+struct OutView {                // per-ticket outputs (any may be null); x per problem
+  double* objective;
+  int32_t *status, *iters, *n_factor;
+  double* nlp_error;
+  int32_t* n_resto;
+};
+
+// Next ticket of this wave and its problem index (uniform); false = retire.
+__device__ __forceinline__ bool claim(const WorkSrc& w, long long& t, long long& pid) {
+  long long v = 0;
+  if (threadIdx.x == 0) v = (long long)__hip_atomic_fetch_add(w.next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __shfl(v, 0, 64);
+  if (!w.q) {
+    pid = t;
+    return t < w.n_static;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&w.q->claimed, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const long long t0 = (long long)wall_clock64();
+  int ok = 0;
+  for (;;) {
+    const long long av = __hip_atomic_load(&w.q->avail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t < av) { ok = 1; break; }
+    if (__hip_atomic_load(&w.q->closed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) {
+      // closed after the last publish: re-read avail once (publish precedes close)
+      ok = t < __hip_atomic_load(&w.q->avail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    if ((long long)wall_clock64() - t0 > w.max_wait) break;   // host gone: retire
+    __builtin_amdgcn_s_sleep(127);
+  }
+  ok = __shfl(ok, 0, 64);
+  if (!ok) return false;
+  int it = 0;
+  if (threadIdx.x == 0) it = __hip_atomic_load(&w.q->items[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  pid = __shfl(it, 0, 64);
+  return true;
+}
+
+// One wavefront per problem at a time; each wave keeps claiming tickets until
+// its work source is exhausted, so a long solve holds one wave and never the
+// launch (no per-launch tail); the workspace is per wave, not per problem.
 template <int EN, int EM>
 __global__ __launch_bounds__(64, HTP_WAVES_PER_EU) void obca_solve_kernel(const Shape* __restrict__ shp, BatchView b,
                                                         double* __restrict__ ws_all, int64_t ws_stride,
                                                         Result* __restrict__ res, double* __restrict__ xout,
-                                                        int batch) {
+                                                        WorkSrc src, OutView ov) {
   __shared__ double lds_[LDS_D];
   __shared__ int ilds_[2 * NBMAX];
   DevWave::ld* lds = (DevWave::ld*)lds_;
   DevWave::li* ilds = (DevWave::li*)ilds_;
-  const int p = blockIdx.x;
-  if (p >= batch) return;
-  DevWave c{(int)threadIdx.x, lds, ilds};
   using CS = DevWave::cst<Shape>;
   CS* sh = (CS*)shp;
-  ProblemIn in = problem_view(b, sh->D, p);
-  double* ws = ws_all + (int64_t)p * ws_stride;
-  ObcaSolver<DevWave, EN, EM> S(c, sh->D, sh->L, sh->o, in, ws);
-  Result r{};
-  S.run(r);
-  if (threadIdx.x == 0) res[p] = r;
-  const double* x = ws + sh->L.x;
-  const int n = sh->D.n;
-  for (int q = threadIdx.x; q < n; q += 64) xout[(int64_t)p * n + q] = x[q];
+  double* ws = ws_all + (int64_t)blockIdx.x * ws_stride;
+  long long t, p;
+  while (claim(src, t, p)) {
+    DevWave c{(int)threadIdx.x, lds, ilds};
+    ProblemIn in = problem_view(b, sh->D, p);
+    ObcaSolver<DevWave, EN, EM> S(c, sh->D, sh->L, sh->o, in, ws);
+    Result r{};
+    S.run(r);
+    if (threadIdx.x == 0) {
+      if (res) res[t] = r;
+      if (ov.objective) ov.objective[t] = r.objective;
+      if (ov.status) ov.status[t] = r.status;
+      if (ov.iters) ov.iters[t] = r.iters;
+      if (ov.n_factor) ov.n_factor[t] = r.n_factor;
+      if (ov.nlp_error) ov.nlp_error[t] = r.nlp_error;
+      if (ov.n_resto) ov.n_resto[t] = r.n_resto;
+    }
+    const double* x = ws + sh->L.x;
+    const int n = sh->D.n;
+    for (int q = threadIdx.x; q < n; q += 64) xout[p * n + q] = x[q];
+    c.sync();
+  }
 }
 
 // point formulation (optimizer_points.py): the same IPM, lambda-only local blocks
@@ -144,6 +215,7 @@ htp_ctx* htp_create(int32_t device) {
 void htp_destroy(htp_ctx* c) {
   if (!c) return;
   if (c->ws) (void)hipFree(c->ws);
+  if (c->next) (void)hipFree(c->next);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->shape) (void)hipFree(c->shape);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -190,48 +262,158 @@ int htp_last_cycles(htp_ctx* ctx, int64_t* out, int32_t batch) {
   return 0;
 }
 
-int htp_obca_solve_batch_device(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result* out, void* stream) {
-  if (!ctx || !in || !out) return -1;
-  const char* e = nullptr;
-  if (check_shape(in, &e)) return fail(ctx, e);
-  if (in->batch == 0) return 0;
-  HIPCHK(hipSetDevice(ctx->device));
+}  // extern "C"
+
+struct htp_queue {
+  htp_ctx* ctx;
+  QueueHost* h;                 // hipHostMalloc (coherent)
+  unsigned long long* next;     // device ticket counter
+  int64_t cap;
+  int64_t limit;                // problems resident for the launch (publish checks pid < limit)
+};
+
+namespace {
+
+template <int EN, int EM>
+int resident_waves_t(htp_ctx* ctx, unsigned pad) {
+  int per_cu = 0, cus = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)obca_solve_kernel<EN, EM>, 64, pad));
+  HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  return per_cu * cus > 0 ? per_cu * cus : 1;
+}
+
+bool uniform44(const Dims& D) {
+  bool u = true;
+  for (int m = 0; m < D.M; ++m) u = u && D.eo[m] == 4;
+  for (int k = 0; k < D.K; ++k) u = u && D.eb[k] == 4;
+  return u;
+}
+
+// Shared launch path of the static-range and queue modes.
+int launch_solve(htp_ctx* ctx, const htp_obca_batch* in, const htp_obca_result* out, hipStream_t s, WorkSrc src,
+                 int64_t waves, bool keep_results) {
   Dims D;
   make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
   Layout L = make_layout(D);
-  const size_t need = (size_t)L.total * sizeof(double) * (size_t)in->batch;
-  if (ensure(ctx, &ctx->ws, &ctx->ws_bytes, need)) return -1;
-  if (ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, sizeof(Result) * (size_t)in->batch)) return -1;
+  const bool u44 = uniform44(D);
+  const unsigned pad = lds_pad_bytes();
+  const int cap = u44 ? resident_waves_t<4, 4>(ctx, pad) : resident_waves_t<MAXE, MAXE>(ctx, pad);
+  if (cap < 0) return -1;
+  if (waves <= 0 || waves > cap) waves = cap;
+  if (src.q == nullptr && waves > src.n_static) waves = src.n_static;
+  if (waves < 1) waves = 1;
+  if (ensure(ctx, &ctx->ws, &ctx->ws_bytes, (size_t)L.total * sizeof(double) * (size_t)waves)) return -1;
+  if (keep_results && ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, sizeof(Result) * (size_t)in->batch)) return -1;
   if (!ctx->shape) HIPCHK(hipMalloc((void**)&ctx->shape, sizeof(Shape)));
   Shape hs{D, L, ctx->opt};
   hs.o.wall_rate = ctx->wall_rate;
   BatchView b{in->traj, in->obs_A, in->obs_b, in->body_G, in->body_g, in->params,
               in->init_control, in->init_mu, in->init_lambda};
-  hipStream_t s = (hipStream_t)stream;
+  OutView ov{out->objective, out->status, out->iterations, out->n_factor, out->nlp_error, out->n_resto};
   HIPCHK(hipMemcpyAsync(ctx->shape, &hs, sizeof(Shape), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(src.next, 0, sizeof(unsigned long long), s));
   HIPCHK(hipEventRecord(ctx->ev0, s));
-  bool u44 = true;
-  for (int m = 0; m < D.M; ++m) u44 = u44 && D.eo[m] == 4;
-  for (int k = 0; k < D.K; ++k) u44 = u44 && D.eb[k] == 4;
-  const unsigned pad = lds_pad_bytes();
+  Result* res = keep_results ? (Result*)ctx->scratch : nullptr;
   if (u44) {
     if (pad) HIPCHK(hipFuncSetAttribute((const void*)obca_solve_kernel<4, 4>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad));
-    hipLaunchKernelGGL((obca_solve_kernel<4, 4>), dim3(in->batch), dim3(64), pad, s, (const Shape*)ctx->shape, b,
-                       (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
+    hipLaunchKernelGGL((obca_solve_kernel<4, 4>), dim3((unsigned)waves), dim3(64), pad, s, (const Shape*)ctx->shape, b,
+                       (double*)ctx->ws, (int64_t)L.total, res, out->x, src, ov);
   } else {
     if (pad) HIPCHK(hipFuncSetAttribute((const void*)obca_solve_kernel<MAXE, MAXE>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad));
-    hipLaunchKernelGGL((obca_solve_kernel<MAXE, MAXE>), dim3(in->batch), dim3(64), pad, s, (const Shape*)ctx->shape, b,
-                       (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
+    hipLaunchKernelGGL((obca_solve_kernel<MAXE, MAXE>), dim3((unsigned)waves), dim3(64), pad, s,
+                       (const Shape*)ctx->shape, b, (double*)ctx->ws, (int64_t)L.total, res, out->x, src, ov);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1, s));
-  hipLaunchKernelGGL(unpack_results, dim3((in->batch + 255) / 256), dim3(256), 0, s, (const Result*)ctx->scratch,
-                     in->batch, out->objective, out->status, out->iterations, out->n_factor, out->nlp_error,
-                     out->n_resto);
-  HIPCHK(hipGetLastError());
   return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t htp_obca_resident_waves(htp_ctx* ctx, const htp_obca_batch* in) {
+  if (!ctx || !in) return -1;
+  const char* e = nullptr;
+  if (check_shape(in, &e)) return fail(ctx, e);
+  Dims D;
+  make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
+  HIPCHK(hipSetDevice(ctx->device));
+  return uniform44(D) ? resident_waves_t<4, 4>(ctx, lds_pad_bytes()) : resident_waves_t<MAXE, MAXE>(ctx, lds_pad_bytes());
+}
+
+int htp_obca_solve_batch_device(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result* out, void* stream) {
+  if (!ctx || !in || !out) return -1;
+  const char* e = nullptr;
+  if (check_shape(in, &e)) return fail(ctx, e);
+  if (in->batch == 0) return 0;
+  if (!out->x) return fail(ctx, "[OBCA] out->x is required");
+  HIPCHK(hipSetDevice(ctx->device));
+  if (!ctx->next) HIPCHK(hipMalloc((void**)&ctx->next, 256));
+  WorkSrc src{(unsigned long long*)ctx->next, nullptr, (long long)in->batch, 0};
+  return launch_solve(ctx, in, out, (hipStream_t)stream, src, 0, true);
+}
+
+htp_queue* htp_queue_create(htp_ctx* ctx, int64_t capacity) {
+  if (!ctx || capacity < 1 || capacity > (int64_t)1 << 31) return nullptr;
+  if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
+  htp_queue* q = new htp_queue{ctx, nullptr, nullptr, capacity, INT64_MAX};
+  const size_t bytes = sizeof(QueueHost) + sizeof(int) * (size_t)capacity;
+  if (hipHostMalloc((void**)&q->h, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipMalloc((void**)&q->next, 256) != hipSuccess) {
+    ctx->err = "htp_queue_create: allocation failed";
+    htp_queue_destroy(q);
+    return nullptr;
+  }
+  std::memset((void*)q->h, 0, bytes);
+  return q;
+}
+
+void htp_queue_destroy(htp_queue* q) {
+  if (!q) return;
+  if (q->h) (void)hipHostFree(q->h);
+  if (q->next) (void)hipFree(q->next);
+  delete q;
+}
+
+int htp_queue_publish(htp_queue* q, const int32_t* pids, int64_t n) {
+  if (!q || n < 0 || (n && !pids)) return -1;
+  if (__atomic_load_n(&q->h->closed, __ATOMIC_ACQUIRE)) return -1;
+  const long long av = __atomic_load_n(&q->h->avail, __ATOMIC_RELAXED);
+  if (av + n > q->cap) return -1;
+  for (int64_t k = 0; k < n; ++k)
+    if (pids[k] < 0 || pids[k] >= q->limit) return -1;
+  std::memcpy(&q->h->items[av], pids, sizeof(int32_t) * (size_t)n);
+  __atomic_store_n(&q->h->avail, av + n, __ATOMIC_RELEASE);
+  return 0;
+}
+
+int htp_queue_close(htp_queue* q) {
+  if (!q) return -1;
+  __atomic_store_n(&q->h->closed, 1, __ATOMIC_RELEASE);
+  return 0;
+}
+
+int64_t htp_queue_published(const htp_queue* q) { return q ? __atomic_load_n(&q->h->avail, __ATOMIC_ACQUIRE) : -1; }
+int64_t htp_queue_claimed(const htp_queue* q) { return q ? __atomic_load_n(&q->h->claimed, __ATOMIC_ACQUIRE) : -1; }
+
+int htp_obca_solve_queue_device(htp_ctx* ctx, const htp_obca_batch* in, htp_queue* q, htp_obca_result* out,
+                                void* stream, int32_t waves, double max_wait_s) {
+  if (!ctx || !in || !q || !out) return -1;
+  const char* e = nullptr;
+  if (check_shape(in, &e)) return fail(ctx, e);
+  if (!out->x) return fail(ctx, "[OBCA] out->x is required");
+  if (q->ctx->device != ctx->device) return fail(ctx, "htp_obca_solve_queue_device: queue of another device");
+  const int64_t av = htp_queue_published(q);
+  for (int64_t t = 0; t < av; ++t)
+    if (q->h->items[t] < 0 || q->h->items[t] >= in->batch) return fail(ctx, "[OBCA] queued problem index out of range");
+  q->limit = in->batch;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (!(max_wait_s > 0)) max_wait_s = 60.0;
+  WorkSrc src{q->next, (QueueHost*)q->h, 0, (long long)(max_wait_s * ctx->wall_rate)};
+  return launch_solve(ctx, in, out, (hipStream_t)stream, src, waves, false);
 }
 
 int htp_obca_solve_batch(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result* out) {

@@ -3,8 +3,10 @@
 Problems are independent, so rank r of W solves a contiguous slice of the
 global id range [0, B) (rank_slice: sizes differ by at most one).  Problem ids seed the
 generator (Philox key [20251015, pid]), so a problem is identical at any world
-size.  The only collectives are the timing barrier and these two tiny
-reductions (RCCL on GPUs, gloo on CPU); nothing is exchanged on the data path.
+size.  rank_slice is each rank's starting share; scheduler.py moves tail chunks
+between ranks (work stealing over an all-gather of next-chunk counters).  The
+other collectives are the timing barrier and these tiny reductions (RCCL on
+GPUs, gloo on CPU); no problem data crosses GPUs.
 """
 
 
@@ -29,3 +31,13 @@ def reduce_stats(dist, device, elapsed, iters_sum, ok_sum):
     s = torch.tensor([float(iters_sum), float(ok_sum)], dtype=torch.float64, device=device)
     dist.all_reduce(s)
     return float(t.item()), float(s[0].item()), float(s[1].item())
+
+
+def sum_ints(dist, device, vals):
+    """Sum of a few integers over ranks."""
+    if dist is None:
+        return [int(v) for v in vals]
+    import torch
+    t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=device)
+    dist.all_reduce(t)
+    return [int(v) for v in t.tolist()]

@@ -99,6 +99,33 @@ double htp_last_kernel_ms(htp_ctx* ctx);
  * local sweeps, assembly, stage chain, KKT solves, total, errors+grad_lag, line search, update. */
 int htp_last_cycles(htp_ctx* ctx, int64_t* out, int32_t batch);
 
+/* Work queue of problem indices feeding ONE persistent solve launch (no
+ * reference counterpart: the reference solves one problem per Python call;
+ * this is the batch runtime behind bench.py's multi-GPU work stealing,
+ * SURVEY.md 8(e)).  The queue lives in pinned, GPU-coherent host memory: the
+ * host appends problem indices and closes it; each wavefront of the running
+ * launch claims the next ticket with a device atomic, waits until that ticket
+ * is published (or the queue is closed: then it retires), and solves problem
+ * items[ticket].  Per-ticket results go to out->objective/status/... [ticket];
+ * out->x is indexed by problem.  A wave that waits longer than
+ * `max_wait_s` for a ticket retires (status of that ticket stays unwritten). */
+typedef struct htp_queue htp_queue;
+htp_queue* htp_queue_create(htp_ctx* ctx, int64_t capacity);
+void htp_queue_destroy(htp_queue* q);
+/* Append problem indices (0 <= pid < batch of the launch); -1 when full / closed. */
+int htp_queue_publish(htp_queue* q, const int32_t* pids, int64_t n);
+int htp_queue_close(htp_queue* q);
+int64_t htp_queue_published(const htp_queue* q);
+/* Tickets claimed so far by the launch's waves (a monotone lower bound). */
+int64_t htp_queue_claimed(const htp_queue* q);
+/* Enqueue the persistent launch on `stream` over the device-resident inputs of
+ * `in` (in->batch = number of resident problems); `waves` = wavefronts in the
+ * launch (<= 0: as many as fit on the device at once). */
+int htp_obca_solve_queue_device(htp_ctx* ctx, const htp_obca_batch* in, htp_queue* q, htp_obca_result* out,
+                                void* stream, int32_t waves, double max_wait_s);
+/* Wavefronts of the OBCA solve kernel resident on the device at once. */
+int32_t htp_obca_resident_waves(htp_ctx* ctx, const htp_obca_batch* in);
+
 /* ---------------------------------------------------------------------------
  * Point formulation (R/obca_py/optimizer_points.py OBCAOptimizer: initialize_manual
  * :52-108, generate_object :193-227, generate_variable :229-255, generate_constrain
