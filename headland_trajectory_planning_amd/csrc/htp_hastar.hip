@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <string>
 
 #define HTP_HD __host__ __device__
@@ -86,11 +87,15 @@ __device__ bool valid(const Pools& P, const double* prm, const int32_t* d, int m
   return true;
 }
 
-// One instantiation per motion type (King: Reeds-Shepp goal shots, Pawn:
-// Dubins + spline); each launch covers the whole batch and a search is run by
-// the instantiation of its own type (searches with an invalid type by King's,
-// which reports them as bad input).
-template <bool KING>
+// One instantiation per motion type (MODE 1 King: Reeds-Shepp goal shots,
+// MODE 0 Pawn: Dubins + spline); each launch covers the whole batch and a
+// search is run by the instantiation of its own type (searches with an invalid
+// type by King's, which reports them as bad input).  MODE 2 is the combined
+// kernel (both goal shots in one body, Search::run dispatch): the default, one
+// launch for a mixed batch (256 VGPRs, no VGPR spills).  The split pair stays
+// selectable (HTP_HA_SPLIT=1) and tests/test_gpu_hastar.py checks that both
+// give the same results on a mixed King/Pawn batch.
+template <int MODE>
 __global__ __launch_bounds__(64) void hastar_kernel(Pools P, int batch, int max_nodes_cap, char* ws, Sizes z,
                                                     htp_hastar_result out, int cap_path, int cap_log) {
   __shared__ Shared sh;
@@ -98,7 +103,8 @@ __global__ __launch_bounds__(64) void hastar_kernel(Pools P, int batch, int max_
   if (b >= batch) return;
   const double* prm = P.params + (int64_t)b * HTP_HA_NPARAM;
   const int32_t* d = P.desc + (int64_t)b * HTP_HA_NDESC;
-  if ((d[D_KING] != 0) != KING) return;
+  constexpr bool KING = MODE == 1;
+  if (MODE != 2 && (d[D_KING] != 0) != KING) return;
   DevWave c{(int)threadIdx.x, nullptr, nullptr};
   Out o{};
   int n_path = 0;
@@ -108,12 +114,17 @@ __global__ __launch_bounds__(64) void hastar_kernel(Pools P, int batch, int max_
     Work w = work_of(ws, z, b);
     Search<DevWave> S(c, prm, d, P.g, w, sh);
     int32_t* log = out.expanded ? out.expanded + (int64_t)b * cap_log * 3 : nullptr;
-    S.template run_t<KING>(o, log, log ? cap_log : 0);
+    if constexpr (MODE == 2) S.run(o, log, log ? cap_log : 0);
+    else S.template run_t<KING>(o, log, log ? cap_log : 0);
     if (o.status == ST_FOUND || o.status == ST_NO_PATH || o.status == ST_MAX_NODES) {
       const int64_t off = (int64_t)b * cap_path;
       int st = o.status;
-      n_path = S.template backtrack_t<KING>(w.hslot, w.cap_node, out.x + off, out.y + off, out.yaw + off, out.dir + off, out.k + off,
-                           cap_path, st);
+      if constexpr (MODE == 2)
+        n_path = S.backtrack(w.hslot, w.cap_node, out.x + off, out.y + off, out.yaw + off, out.dir + off, out.k + off,
+                             cap_path, st);
+      else
+        n_path = S.template backtrack_t<KING>(w.hslot, w.cap_node, out.x + off, out.y + off, out.yaw + off,
+                                              out.dir + off, out.k + off, cap_path, st);
       o.status = st;
     }
   }
@@ -130,12 +141,19 @@ int enqueue(htp_ctx* ctx, const htp_hastar_batch* in, const Pools& P, htp_hastar
   const Sizes z = ws_sizes(in->max_nodes_cap);
   if (ensure(ctx, &ctx->ha_ws, &ctx->ha_ws_bytes, z.per_search * (size_t)in->batch)) return -1;
   HIPCHK(hipEventRecord(ctx->ha_ev0, s));
-  hipLaunchKernelGGL(hastar_kernel<true>, dim3(in->batch), dim3(64), 0, s, P, in->batch, in->max_nodes_cap,
-                     (char*)ctx->ha_ws, z, out, in->cap_path, out.expanded ? in->cap_log : 0);
-  HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(hastar_kernel<false>, dim3(in->batch), dim3(64), 0, s, P, in->batch, in->max_nodes_cap,
-                     (char*)ctx->ha_ws, z, out, in->cap_path, out.expanded ? in->cap_log : 0);
-  HIPCHK(hipGetLastError());
+  const char* split = getenv("HTP_HA_SPLIT");
+  if (!(split && split[0] == '1')) {
+    hipLaunchKernelGGL(hastar_kernel<2>, dim3(in->batch), dim3(64), 0, s, P, in->batch, in->max_nodes_cap,
+                       (char*)ctx->ha_ws, z, out, in->cap_path, out.expanded ? in->cap_log : 0);
+    HIPCHK(hipGetLastError());
+  } else {
+    hipLaunchKernelGGL(hastar_kernel<1>, dim3(in->batch), dim3(64), 0, s, P, in->batch, in->max_nodes_cap,
+                       (char*)ctx->ha_ws, z, out, in->cap_path, out.expanded ? in->cap_log : 0);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(hastar_kernel<0>, dim3(in->batch), dim3(64), 0, s, P, in->batch, in->max_nodes_cap,
+                       (char*)ctx->ha_ws, z, out, in->cap_path, out.expanded ? in->cap_log : 0);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipEventRecord(ctx->ha_ev1, s));
   return 0;
 }

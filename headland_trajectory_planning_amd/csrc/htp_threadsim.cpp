@@ -8,70 +8,10 @@
 #define HTP_HD
 #include "wave_ctx.h"
 #include "obca_batch.h"
+#include "thread_wave.h"
 
 using namespace htp;
 
-namespace {
-struct Shared {
-  std::barrier<> bar{64};
-  double red[64];
-  int ired[64];
-};
-struct ThreadWave {
-  using gd = double;
-  using ld = double;
-  using li = int;
-  template <class T>
-  using cst = const T;
-  static constexpr int width = 64;
-  static constexpr bool kMfma = false;
-  int lane;
-  double* lds;
-  int* ildsp;
-  Shared* sh;
-  void sync() const { sh->bar.arrive_and_wait(); }
-  double sum(double v) const {
-    sync();
-    sh->red[lane] = v;
-    sync();
-    double s = 0;
-    for (int i = 0; i < 64; ++i) s += sh->red[i];
-    sync();
-    return s;
-  }
-  double maxv(double v) const {
-    sync(); sh->red[lane] = v; sync();
-    double s = sh->red[0];
-    for (int i = 1; i < 64; ++i) s = fmax(s, sh->red[i]);
-    sync();
-    return s;
-  }
-  double minv(double v) const {
-    sync(); sh->red[lane] = v; sync();
-    double s = sh->red[0];
-    for (int i = 1; i < 64; ++i) s = fmin(s, sh->red[i]);
-    sync();
-    return s;
-  }
-  int isum(int v) const {
-    sync(); sh->ired[lane] = v; sync();
-    int s = 0;
-    for (int i = 0; i < 64; ++i) s += sh->ired[i];
-    sync();
-    return s;
-  }
-  long long clock() const { return 0; }
-  long long wall() const { return 0; }
-  double uniform(double v) const { return v; }
-  int uniform_i(int v) const { return v; }
-  double bcast(double v, int src) const {
-    sync(); sh->red[lane] = v; sync();
-    double r = sh->red[src];
-    sync();
-    return r;
-  }
-};
-}  // namespace
 
 extern "C" int htp_threadsim_obca_solve(const htp_obca_batch* in, htp_obca_result* out, int max_iter) {
   const char* e = nullptr;
@@ -87,7 +27,7 @@ extern "C" int htp_threadsim_obca_solve(const htp_obca_batch* in, htp_obca_resul
     std::vector<double> ws((size_t)L.total, 0.0);
     std::vector<double> lds(4 * NBMAX * NBMAX + 8 + 128, 0.0);
     std::vector<int> ilds(2 * NBMAX, 0);
-    Shared sh;
+    WaveShared sh;
     std::vector<Result> rr(64);
     std::vector<std::thread> th;
     for (int lane = 0; lane < 64; ++lane)

@@ -70,3 +70,20 @@ def test_dropin_shim_search_and_batch(ctx):
     assert np.allclose(xs, o["xs"], atol=1e-9) and np.allclose(ks, o["ks"], atol=1e-9)
     out = hybrid_a_star_search_batch([hs, hs], max_nodes=60)
     assert out[0][5] == out[1][5] == counter
+
+
+def test_combined_king_pawn_kernel_matches_split_kernels(ctx, monkeypatch):
+    """Round-1 note: a combined King+Pawn kernel once returned wrong
+    Pawn statuses.  The combined body (Search::run dispatch, the default) must
+    give the split kernels' results (HTP_HA_SPLIT=1) on a mixed batch, and the
+    host build's."""
+    probs = [U.scenario_pawn(s, n_obs=1 + s % 3) for s in range(16)] + [U.scenario(s, max_nodes=80) for s in range(16)]
+    probs = [p for pair in zip(probs[:16], probs[16:]) for p in pair]
+    comb = _gpu(ctx, probs)
+    monkeypatch.setenv("HTP_HA_SPLIT", "1")
+    split = _gpu(ctx, probs)
+    monkeypatch.delenv("HTP_HA_SPLIT")
+    host = H.as_dicts(H.hastar_host(probs))
+    for a, b, h in zip(split, comb, host):
+        assert U.compare(a, b, exact=False, tol=1e-12) == []
+        assert U.compare(h, b, exact=False) == []
