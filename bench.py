@@ -37,25 +37,31 @@ OUT_KEYS = ("objective", "status", "iterations", "n_factor", "nlp_error", "n_res
 
 
 def _gen(args):
-    pid, N, M, imp = args
-    return synth.make_instance(pid, N=N, M=M, implement=imp)
+    pid, cfg = args
+    return synth.config_instance(cfg, pid)
 
 
-def make_batch(pids, N, M, imp, procs=16):
+def make_batch(pids, cfg, procs=16):
+    """Instances of config `cfg` (shape, implement and turn type: synth.TURNS) for problem ids `pids`."""
     if len(pids) <= 64 or procs <= 1:
-        return [_gen((p, N, M, imp)) for p in pids]
+        return [_gen((p, cfg)) for p in pids]
     import multiprocessing as mp
     nproc = max(1, min(procs, (os.cpu_count() or 4)))
     with mp.get_context("fork").Pool(nproc) as pool:
-        return pool.map(_gen, [(p, N, M, imp) for p in pids], chunksize=32)
+        return pool.map(_gen, [(p, cfg) for p in pids], chunksize=32)
 
 
-def make_global_batch(GB, N, M, imp, rank, world, dist, procs):
+def make_global_batch(GB, cfg, rank, world, dist, procs):
     """Every rank needs every problem's inputs (a stolen chunk can be any
     problem): rank r generates its slice, the slices are exchanged through
     files under /dev/shm (not a device collective), then each rank packs all."""
     pids = sharding.rank_slice(rank, world, GB)
-    own = _native.PackedBatch(make_batch(pids, N, M, imp, procs))
+    insts = make_batch(pids, cfg, procs)
+    turns = {}
+    for inst in insts:
+        turns[inst["meta"]["turn"]] = turns.get(inst["meta"]["turn"], 0) + 1
+    own = _native.PackedBatch(insts)
+    own.turns = turns
     if world == 1:
         return own
     tag = os.environ.get("MASTER_PORT", "0")
@@ -76,7 +82,9 @@ def make_global_batch(GB, N, M, imp, rank, world, dist, procs):
         parts.append(p)
     dist.barrier()
     os.unlink(path(rank))
-    return _native.PackedBatch.concat(parts)
+    out = _native.PackedBatch.concat(parts)
+    out.turns = turns
+    return out
 
 
 def _cpu_model():
@@ -161,7 +169,7 @@ def main():
     Bcfg, N, M, imp = synth.CONFIGS[args.config]
     GB = args.batch or Bcfg
     t = time.perf_counter()
-    pk = make_global_batch(GB, N, M, imp, rank, world, dist, args.gen_procs)
+    pk = make_global_batch(GB, args.config, rank, world, dist, args.gen_procs)
     gen_s = time.perf_counter() - t
 
     dev_in = {k: torch.from_numpy(getattr(pk, k)).to(dev) for k in pk.INPUTS if getattr(pk, k) is not None}
@@ -268,7 +276,7 @@ def main():
     if mf and os.path.exists(mf):
         mj = json.load(open(mf))
         if mj.get("solver_sha") == _native.core_sha():
-            mfma = {k: mj[k] for k in ("mfma_f64_per_problem_iter", "mfma_busy_frac", "valu_per_problem_iter")
+            mfma = {k: mj[k] for k in ("mfma_f64_per_problem_iter", "mfma_busy_frac", "mfma_f64_tflops", "mfma_f64_frac_of_peak", "valu_per_problem_iter")
                     if k in mj}
 
     line = {
@@ -279,7 +287,8 @@ def main():
         "config": {"workload": f"config {args.config}: global batch {GB} split over {world} GPU(s), "
                                f"N={N} horizon, M={M} obstacles, K={pk.K} bodies ({imp}), time-opt on; "
                                f"IPOPT-restated IPM to tol 1e-8",
-                   "global_batch": GB, "N": N, "M": M, "K": pk.K,
+                   "global_batch": GB, "N": N, "M": M, "K": pk.K, "turn_types": synth.TURNS[args.config],
+                   "turn_histogram_rank0_slice": getattr(pk, "turns", None),
                    "parallelism": f"problem-sharded x{world}, work stealing"},
         "execution": {"launch": f"one persistent launch per GPU ({waves} wavefronts) fed by a host work queue",
                       "chunk": args.chunk if world > 1 else GB * args.steps, "chunks_rank0": len(loop.solved),

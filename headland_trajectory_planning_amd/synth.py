@@ -9,11 +9,23 @@ Geometry follows the reference's orchard model:
 * obstacles ............ R/path_planner/OGE_OBCA.py:306-373,477-677: a headland
   boundary quad, the up/low bound quad and tree-row rectangles (SAFETY_BOUND 0.2),
   trimmed / padded to exactly M convex quads (padding: far dummy quads, >= 50 m away)
-* warm start ........... the reference's Dubins fallback
-  (R/path_planner/OBCA_warm_start.py:166-174, pydubins shortest path) sampled to
-  exactly N poses, turned into [x, y, v, theta, steer] as
-  R/obca_py/util.py:62-113 does (v = dir*desired_v, steer = atan(L*kappa),
-  v[0]=v[-1]=steer[0]=0, heading wrapped + unwrapped).
+* warm start ........... one of the reference's turn types (`turn=`):
+  - "dubins": the Dubins fallback (R/path_planner/OBCA_warm_start.py:166-174,
+    pydubins shortest path);
+  - "circleback": the circle-back / Omega turn of
+    R/path_planner/safety_forward_path_plan.py:395-454 (forward arc R_f by
+    theta, reverse arc R_b by pi - theta, Dubins lead-in; radii grow 5 % until
+    the reverse arc ends short of the row; rows wider than 2R fall back to Dubins);
+  - "fishtail": a three-arc C|C|C K-turn (forward, reverse, forward at the
+    minimum radius, symmetric outer arcs) joined to the row poses by straights --
+    the Reeds-Shepp C|C|C family the fish-tail planner
+    (safety_forward_path_plan.py:300-392) picks between offset poses of one x;
+    rows wider than 2R fall back to Dubins;
+  - "mixed": one of the three per problem (its own Philox stream, key + 1).
+  The path is sampled to exactly N poses and turned into [x, y, v, theta, steer]
+  as R/obca_py/util.py:62-113 does (v = dir*desired_v, steer = atan(L*kappa)
+  with kappa the steering curvature, v[0]=v[-1]=steer[0]=0, heading wrapped +
+  unwrapped).
 
 The headland boundary is placed behind the warm start's swept footprint with a
 random margin, so every instance starts collision-free and the boundary is
@@ -115,6 +127,109 @@ def dubins_sample(q0, r, name, seg, s):
     return np.stack([q0[0] + x * r, q0[1] + y * r, th, kap], axis=1)
 
 
+# ------------------------------------------------- arc/straight segment paths
+def segments_sample(q0, segs, s):
+    """Pose, steering curvature and gear at arc lengths s (metres, along |path|) of a
+    path of segments (kappa, u): kappa = steering curvature (dtheta per signed metre),
+    u = signed length (u < 0 drives in reverse).  Returns (P, 5) [x, y, theta, kappa, dir]."""
+    s = np.asarray(s, dtype=np.float64)
+    out = np.zeros((s.size, 5))
+    x, y, th = float(q0[0]), float(q0[1]), float(q0[2])
+    start = 0.0
+    for j, (kap, u) in enumerate(segs):
+        ln = abs(u)
+        sgn = 1.0 if u >= 0 else -1.0
+        last = j == len(segs) - 1
+        sel = (s >= start) & ((s < start + ln) | last)
+        t = np.clip(s[sel] - start, 0.0, ln) * sgn
+        if kap != 0.0:
+            th1 = th + kap * t
+            out[sel, 0] = x + (np.sin(th1) - math.sin(th)) / kap
+            out[sel, 1] = y - (np.cos(th1) - math.cos(th)) / kap
+            out[sel, 2] = th1
+        else:
+            out[sel, 0] = x + t * math.cos(th)
+            out[sel, 1] = y + t * math.sin(th)
+            out[sel, 2] = th
+        out[sel, 3] = kap
+        out[sel, 4] = sgn
+        if kap != 0.0:
+            th1 = th + kap * u
+            x, y = x + (math.sin(th1) - math.sin(th)) / kap, y - (math.cos(th1) - math.cos(th)) / kap
+            th = th1
+        else:
+            x, y = x + u * math.cos(th), y + u * math.sin(th)
+        start += ln
+    return out
+
+
+def _seg_end(q0, segs):
+    return segments_sample(q0, segs, [sum(abs(u) for _, u in segs)])[0]
+
+
+def dubins_segments(q0, q1, r):
+    """Shortest Dubins word as segments (steering curvature +1/r = L)."""
+    name, seg = dubins_shortest(q0, q1, r)
+    return [({"L": 1.0 / r, "R": -1.0 / r, "S": 0.0}[ch], ln * r) for ch, ln in zip(name, seg)]
+
+
+def circle_back_segments(ps, pe, r, step=0.1):
+    """safety_forward_path_plan.py:395-454 (get_circle_back_path_full, NEAR side, exit heading pi,
+    enter heading 0): forward arc (Rf, theta) toward the next rows, reverse arc (Rb, pi - theta),
+    Dubins lead-in to the row pose; None when the rows are 2R or more apart (the reference's Dubins
+    fallback)."""
+    w = abs(pe[1] - ps[1])
+    if w >= 2.0 * r:
+        return None
+    Rf = Rb = r
+    while True:
+        theta = math.pi / 2 + math.asin((Rb + w - Rf) / (Rf + Rb))
+        if ps[0] - (Rf + Rb) * math.cos(theta - math.pi / 2) < pe[0] - step:
+            break
+        Rf *= 1.05
+        Rb *= 1.05
+    turn = 1.0 if pe[1] - ps[1] > 0 else -1.0   # steer sign of get_steer_dir_for_enter_calculation (heading pi)
+    segs = [(-turn / Rf, Rf * theta), (turn / Rb, -Rb * (math.pi - theta))]
+    q = _seg_end(ps, segs)
+    return segs + [sg for sg in dubins_segments((q[0], q[1], q[2]), pe, r) if sg[1] > 1e-12]
+
+
+def fishtail_segments(ps, pe, r):
+    """Three-arc C|C|C K-turn at the minimum radius: forward arc a, reverse arc pi - 2a, forward
+    arc a (heading pi -> 0), a chosen by bisection so the lateral shift equals the row offset, then
+    straights along the row axis so it starts at the exit pose and ends at the enter pose.  None
+    when the rows are 2R or more apart."""
+    w = pe[1] - ps[1]
+    turn = 1.0 if w > 0 else -1.0
+    if abs(w) >= 2.0 * r:
+        return None
+
+    def arcs(a):
+        return [(-turn / r, r * a), (turn / r, -r * (math.pi - 2 * a)), (-turn / r, r * a)]
+
+    lo, hi = 0.0, math.pi / 2   # signed lateral shift grows from -2r (a = 0) to 2r (a = pi/2)
+    for _ in range(80):
+        mid = 0.5 * (lo + hi)
+        dy = _seg_end((0.0, 0.0, ps[2]), arcs(mid))[1]
+        if turn * dy < abs(w):
+            lo = mid
+        else:
+            hi = mid
+    segs = arcs(0.5 * (lo + hi))
+    dx = _seg_end((0.0, 0.0, ps[2]), segs)[0]
+    lead = ps[0] + dx - pe[0]            # forward along heading pi before the arcs (moves -x)
+    out = []
+    if lead > 0:
+        out.append((0.0, lead))
+    out += segs
+    if lead < 0:
+        out.append((0.0, -lead))          # forward along heading 0 after the arcs
+    return out
+
+
+TURN_TYPES = ("dubins", "circleback", "fishtail")
+
+
 # ------------------------------------------------------------ angle helpers
 def wrap_angle(a):
     """R/obca_py/util.py:7-13 (Python floored modulo)."""
@@ -162,9 +277,14 @@ def _rect(x0, x1, y0, y1):
 
 
 # ---------------------------------------------------------------- instance
-def make_instance(pid, N=80, M=6, implement="none", key=20251015, **over):
-    """One OBCA instance (oracle/nlp.py instance format) for problem id `pid`."""
+def make_instance(pid, N=80, M=6, implement="none", key=20251015, turn="dubins", **over):
+    """One OBCA instance (oracle/nlp.py instance format) for problem id `pid`; `turn` is one of
+    TURN_TYPES or "mixed" (see the module docstring)."""
     rng = np.random.Generator(np.random.Philox(key=[key, pid]))
+    if turn == "mixed":
+        turn = TURN_TYPES[int(np.random.Generator(np.random.Philox(key=[key + 1, pid])).integers(0, 3))]
+    if turn not in TURN_TYPES:
+        raise ValueError("unknown turn type %r" % (turn,))
     veh = dict(VEHICLE)
     r_min = veh["wheelbase"] / math.tan(veh["max_steer"])
     body = geometry.body_rectangle(veh["axle_to_front"], veh["axle_to_back"], veh["width"])
@@ -183,6 +303,8 @@ def make_instance(pid, N=80, M=6, implement="none", key=20251015, **over):
         ys0 = row_w * np.arange(rows)
         s_row = int(rng.integers(0, 5))
         e_row = min(s_row + int(rng.integers(1, 4)), rows - 2)
+        if turn != "dubins":   # fish-tail / circle-back turns go to the adjacent row
+            e_row = s_row + 1
         exit_off = rng.uniform(-1.0, 1.0)
         enter_off = rng.uniform(0.0, 3.66)
         margin = rng.uniform(0.3, 1.0)
@@ -192,9 +314,23 @@ def make_instance(pid, N=80, M=6, implement="none", key=20251015, **over):
         pe = near(e_row) - np.array([1.0, 0.0]) * enter_off   # ENTER, yaw = 0
         q0 = (ps[0], ps[1], math.pi)
         q1 = (pe[0], pe[1], 0.0)
-        name, seg = dubins_shortest(q0, q1, r_min)
-        Lp = sum(seg) * r_min
-        smp = dubins_sample(q0, r_min, name, seg, np.linspace(0.0, Lp, N))
+        segs = None
+        if turn == "circleback":
+            segs = circle_back_segments(q0, q1, r_min)
+        elif turn == "fishtail":
+            segs = fishtail_segments(q0, q1, r_min)
+        if segs is None:   # "dubins", or rows 2R or more apart (the reference's Dubins fallback)
+            used = "dubins"
+            name, seg = dubins_shortest(q0, q1, r_min)
+            Lp = sum(seg) * r_min
+            smp = dubins_sample(q0, r_min, name, seg, np.linspace(0.0, Lp, N))
+            gear = np.ones(N)
+        else:
+            used = turn
+            name = "".join("S" if k == 0.0 else ("L" if k > 0 else "R") + ("-" if u < 0 else "+") for k, u in segs)
+            Lp = sum(abs(u) for _, u in segs)
+            smp = segments_sample(q0, segs, np.linspace(0.0, Lp, N))
+            gear = smp[:, 4]
         # footprint of the warm start (every pose, body + implements)
         foot = [_polys_at(p, smp[:, :3]) for p in polys]
         allpts = np.concatenate([f.reshape(-1, 2) for f in foot])
@@ -223,7 +359,7 @@ def make_instance(pid, N=80, M=6, implement="none", key=20251015, **over):
     desired_v = min(ds / dT, 0.9)
     traj = np.zeros((N, 5))
     traj[:, 0], traj[:, 1] = smp[:, 0], smp[:, 1]
-    traj[:, 2] = desired_v
+    traj[:, 2] = desired_v * gear
     traj[:, 3] = process_angle(smp[:, 2])
     traj[:, 4] = np.arctan(veh["wheelbase"] * smp[:, 3])
     traj[0, 2] = traj[-1, 2] = 0.0
@@ -237,7 +373,7 @@ def make_instance(pid, N=80, M=6, implement="none", key=20251015, **over):
         W=DEFAULT_WEIGHTS["W"].copy(), wheelbase=veh["wheelbase"], max_steer=veh["max_steer"],
         max_velocity=1.0, max_accel=1.0, max_steer_rate=0.7, min_dist=0.1,
         x_bound=[-np.inf, np.inf], y_bound=[-np.inf, np.inf],
-        meta=dict(pid=pid, dubins=name, length=Lp, start=q0, goal=q1, s_row=s_row, e_row=e_row),
+        meta=dict(pid=pid, turn=used, dubins=name, length=Lp, start=q0, goal=q1, s_row=s_row, e_row=e_row),
     )
     for kk, vv in over.items():
         inst[kk] = vv
@@ -268,6 +404,16 @@ def make_points_instance(pid, N=80, M=6, implement="none", key=20251015, **over)
     for kk, vv in over.items():
         inst[kk] = vv
     return inst
+
+
+# turn types of the BASELINE configs: A fish-tail, B Omega/circle-back, C mixed, D/E the Dubins turn
+TURNS = {"A": "fishtail", "B": "circleback", "C": "mixed", "D": "dubins", "E": "dubins"}
+
+
+def config_instance(cfg, pid, **over):
+    """Problem `pid` of BASELINE config `cfg` (shape, implement and turn type)."""
+    _, N, M, imp = CONFIGS[cfg]
+    return make_instance(pid, N=N, M=M, implement=imp, turn=TURNS[cfg], **over)
 
 
 CONFIGS = {

@@ -179,3 +179,41 @@ def ypark_dicts(res):
     return [dict(status=int(res.status[b]), cand=int(res.cand[b]), params=res.params[b].tolist(),
                  path=res.path[b, :int(res.n_path[b])].copy(), n_pose=int(res.n_pose[b]))
             for b in range(len(res.status))]
+
+
+ASAN_EXE = os.path.join(ROOT, "build", "hastar_asan")
+
+
+def hastar_asan(problems, cap_path=4096, sanitize=True):
+    """The host build of hastar_core.h (csrc/hastar_asan.cpp) as a standalone executable built
+    with -fsanitize=address,undefined: any out-of-bounds access or UB aborts it.  Same result
+    object as hastar_host.  TEST-ONLY."""
+    import tempfile
+    exe = ASAN_EXE if sanitize else ASAN_EXE + "_plain"
+    src = os.path.join(CSRC, "hastar_asan.cpp")
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + [src]
+    if not (os.path.exists(exe) and os.path.getmtime(exe) >= max(os.path.getmtime(d) for d in deps)):
+        os.makedirs(os.path.dirname(exe), exist_ok=True)
+        flags = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"] \
+            if sanitize else []
+        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17"] + flags + ["-o", exe, src])
+    pk = _native.HastarPacked(problems, cap_path=cap_path)
+    res = _native.HastarResults(pk)
+    with tempfile.TemporaryDirectory() as td:
+        fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
+        with open(fin, "wb") as f:
+            np.array([pk.batch, len(pk.poly_off) - 1, pk.vertices.shape[0], pk.guide.shape[0], pk.motions.shape[0],
+                      pk.max_nodes_cap, pk.cap_path, pk.cap_log], np.int32).tofile(f)
+            for a, t in ((pk.params, np.float64), (pk.desc, np.int32), (pk.poly_off, np.int32),
+                         (pk.vertices, np.float64), (pk.lane_len, np.float64), (pk.guide, np.float64),
+                         (pk.motions, np.float64)):
+                np.ascontiguousarray(a, dtype=t).tofile(f)
+        env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+        p = subprocess.run([exe, fin, fout], env=env, capture_output=True, text=True, timeout=1800)
+        if p.returncode != 0:
+            raise RuntimeError(f"hastar_asan exit {p.returncode}: {p.stderr[-4000:]}")
+        with open(fout, "rb") as f:
+            for n in ("status", "counter", "n_path", "n_expanded", "n_pose", "x", "y", "yaw", "dir", "k", "expanded"):
+                a = getattr(res, n)
+                a[...] = np.fromfile(f, dtype=a.dtype, count=a.size).reshape(a.shape)
+    return res

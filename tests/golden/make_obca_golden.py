@@ -2,13 +2,14 @@
 
 TEST INFRASTRUCTURE: the oracle (oracle/ipm.py IPOPT restatement with the
 structured KKT of oracle/structured.py) solves selected problems of the
-BASELINE configs A-E (synth.make_instance, the same Philox-seeded workload as
-bench.py) on the CPU; each fixture stores the state trajectory (5N), the
+BASELINE configs A-E (synth.config_instance: shape, implement and turn type --
+A fish-tail, B circle-back, C mixed, D/E Dubins -- the same Philox-seeded
+workload as bench.py) on the CPU; each fixture stores the state trajectory (5N), the
 objective, the status, the iteration count and the number of restoration
 phases.  tests/test_gpu_obca.py compares the HIP solver against them (the
 oracle needs minutes to hours per full-size problem, too slow to run inside a
 GPU test).  Several pids are problems whose line search fails and that need
-IPOPT's feasibility restoration (D 33/971, C 47/66, E 12).
+IPOPT's feasibility restoration (D 33/971, C 47, E 12).
 
     python tests/golden/make_obca_golden.py [CFG:PID ...]
 """
@@ -23,7 +24,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tests", "golden", "obca_full")
 
-CASES = ["A:0", "A:1", "A:2", "D:0", "D:33", "D:971", "C:0", "C:47", "C:66", "E:0", "E:1", "E:12"]
+CASES = ["A:0", "A:1", "A:2", "B:0", "B:1", "B:9", "D:0", "D:33", "D:971", "C:0", "C:1", "C:2", "C:47", "E:0", "E:1",
+         "E:12"]
 
 
 def run(case):
@@ -34,12 +36,13 @@ def run(case):
     cfg, pid = case.split(":")
     pid = int(pid)
     _, N, M, imp = synth.CONFIGS[cfg]
-    nlp = ObcaNLP(synth.make_instance(pid, N=N, M=M, implement=imp))
+    inst = synth.config_instance(cfg, pid)
+    nlp = ObcaNLP(inst)
     t = time.time()
     r = IpoptRestatement(nlp, kkt=StructuredKKT(nlp)).solve()
     dt = time.time() - t
     np.savez(os.path.join(OUT, f"{cfg}{pid}.npz"), states=r["x"][:5 * N], f=r["f"], status=r["status"],
-             iters=r["iters"], n_resto=r["n_resto"], N=N, M=M, implement=imp, seconds=dt)
+             iters=r["iters"], n_resto=r["n_resto"], N=N, M=M, implement=imp, turn=inst["meta"]["turn"], seconds=dt)
     return f"{case} {r['status_str']} iters={r['iters']} n_resto={r['n_resto']} f={r['f']:.12g} ({dt:.0f} s)"
 
 

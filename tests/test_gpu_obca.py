@@ -70,7 +70,10 @@ def test_full_config_parity_vs_oracle_fixtures(ctx, cfg, pid, path):
     g = np.load(path)
     _, N, M, imp = synth.CONFIGS[cfg]
     assert int(g["N"]) == N
-    res = ctx.solve(_native.PackedBatch([synth.make_instance(pid, N=N, M=M, implement=imp)]))
+    inst = synth.config_instance(cfg, pid)
+    if "turn" in g.files:
+        assert inst["meta"]["turn"] == str(g["turn"])
+    res = ctx.solve(_native.PackedBatch([inst]))
     assert res.status[0] == int(g["status"]) and res.status[0] in (0, 1), (res.status[0], int(g["status"]))
     assert np.max(np.abs(res.x[0, :5 * N] - g["states"])) <= STATE_TOL
     assert abs(res.objective[0] - float(g["f"])) <= 1e-6 * max(1.0, abs(float(g["f"])))
@@ -105,10 +108,10 @@ def _stationarity(nlp, x, tol_act=1e-3):
     return np.max(np.abs(gf + A @ y)) / max(1.0, np.max(np.abs(gf)))
 
 
-@pytest.mark.parametrize("cfg,nprob,min_ok", [("B", 64, 0.98), ("C", 64, 0.98), ("E", 16, 0.85)])
+@pytest.mark.parametrize("cfg,nprob,min_ok", [("A", 64, 0.98), ("B", 64, 0.98), ("C", 64, 0.98), ("E", 16, 0.85)])
 def test_full_config_properties(ctx, cfg, nprob, min_ok):
-    _, N, M, imp = synth.CONFIGS[cfg]
-    insts = [synth.make_instance(pid, N=N, M=M, implement=imp) for pid in range(nprob)]
+    """Configs at their turn types (A fish-tail, B circle-back, C mixed with the mower)."""
+    insts = [synth.config_instance(cfg, pid) for pid in range(nprob)]
     pk = _native.PackedBatch(insts)
     res = ctx.solve(pk)
     ok = np.isin(res.status, [0, 1])

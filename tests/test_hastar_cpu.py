@@ -115,3 +115,16 @@ def test_host_core_matches_oracle_pawn(seed):
     o = U.run_oracle(p)
     h = H.as_dicts(H.hastar_host([p]))[0]
     assert U.compare(o, h, exact=False, tol=1e-9) == []
+
+
+def test_host_core_under_asan_ubsan_mixed_king_pawn():
+    """the hybrid A* core (King RS shots, Pawn Dubins + spline shots) under
+    AddressSanitizer + UBSan with exact-size buffers: no out-of-bounds access or undefined
+    behaviour, and the same results as the plain host build."""
+    import _hostsim as H
+    import _ha_util as U
+    probs = [U.scenario_pawn(s, n_obs=1 + s % 3) for s in range(12)] + [U.scenario(s, max_nodes=80) for s in range(12)]
+    asan = H.as_dicts(H.hastar_asan(probs))
+    host = H.as_dicts(H.hastar_host(probs))
+    for a, h in zip(asan, host):
+        assert U.compare(h, a, exact=True) == []

@@ -4,7 +4,7 @@ sys.path.insert(0, ".")
 from headland_trajectory_planning_amd import _native  # noqa: E402
 import bench  # noqa: E402
 B = 4096
-pk = _native.PackedBatch(bench.make_batch(list(range(B)), 80, 6, "none", 16))
+pk = _native.PackedBatch(bench.make_batch(list(range(B)), "D", 16))
 res = {}
 for name in ("libhtp.so", "libhtp_w4.so"):
     ctx = _native.Context(0, lib=_native.load(_native.LIB_PATH.replace("libhtp.so", name)))

@@ -11,7 +11,7 @@ import bench  # noqa: E402
 
 B = int(sys.argv[1])
 names = sys.argv[2:]
-insts = bench.make_batch(list(range(B)), 80, 6, "none", 16)
+insts = bench.make_batch(list(range(B)), "D", 16)
 pk = _native.PackedBatch(insts)
 ctxs = {}
 for n in names:

@@ -13,7 +13,7 @@ b, N, M, imp = synth.CONFIGS[cfg]
 import bench
 batch = batch or b
 t = time.time()
-insts = bench.make_batch(list(range(batch)), N, M, imp, 16)
+insts = bench.make_batch(list(range(batch)), cfg, 16)
 print(f"gen {batch} problems: {time.time() - t:.1f}s", flush=True)
 pk = _native.PackedBatch(insts)
 ctx = _native.Context(0)

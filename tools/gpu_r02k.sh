@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-2 evidence on the committed kernel: GPU tests, smoke, default bench line, kernel-trace stats.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+T=${1:-r02k}
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${T}_gputest.log 2>&1
+rc=$?; echo "gputest rc=$rc"; tail -3 gpurun_out/${T}_gputest.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/${T}_smoke.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err
+rc=$?; echo "bench rc=$rc"; cat gpurun_out/${T}_bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_bench.err; exit $rc; }

@@ -12,7 +12,7 @@ import bench  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 caps = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "49152", "65536", "98304", "0"]
-pk = _native.PackedBatch(bench.make_batch(list(range(B)), 80, 6, "none", 16))
+pk = _native.PackedBatch(bench.make_batch(list(range(B)), "D", 16))
 ctx = _native.Context(0)
 ref = None
 for cap in caps:

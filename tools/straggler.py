@@ -9,7 +9,7 @@ from headland_trajectory_planning_amd import _native  # noqa: E402
 import bench  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-insts = bench.make_batch(list(range(B)), 80, 6, "none", 16)
+insts = bench.make_batch(list(range(B)), "D", 16)
 ctx = _native.Context(0)
 names = ["local", "assemble", "chain", "kktsolve", "total", "errors", "linesearch", "update"]
 
