@@ -101,6 +101,7 @@ struct Layout {
   // watchdog reference point and direction (x, s, y, z, v, R, zR, c, d, step)
   int64_t wx, ws, wyc, wyd, wzL, wzU, wvL, wvU, wR, wzR, wc, wd, wdx, wds, wdyc, wdyd, wdR;
   int64_t ax;                                                // last acceptable iterate (x)
+  int64_t plist;                                             // compacted block indices (local sweeps, pass 2)
   int64_t total;
 };
 
@@ -198,6 +199,7 @@ inline Layout make_layout(const Dims& d) {
   L.wvL = take(d.md); L.wvU = take(d.md); L.wR = take(nR); L.wzR = take(nR); L.wc = take(d.mc); L.wd = take(d.md);
   L.wdx = take(d.n); L.wds = take(d.md); L.wdyc = take(d.mc); L.wdyd = take(d.md); L.wdR = take(nR);
   L.ax = take(d.n);
+  L.plist = take(d.P);
   L.total = o;
   return L;
 }

@@ -21,7 +21,7 @@ using namespace htp;
 
 namespace {
 
-constexpr int LDS_D = 4 * NBMAX * NBMAX + 8 + 2 * 64;
+constexpr int LDS_D = RING_OFF + RING_DOUBLES;  // scratch + filter (obca_core.h) + Riccati stage ring
 
 #ifndef HTP_WAVES_PER_EU
 #define HTP_WAVES_PER_EU 1

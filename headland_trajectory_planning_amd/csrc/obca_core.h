@@ -287,6 +287,15 @@ HTP_HD inline void bk_solve_packed(const double* K, const int* ip, int n, double
   }
 }
 
+// LDS ring of the matrix-core Riccati passes (ObcaSolver::ring_fill): RING_SB + 1 stage records of
+// RS_L doubles (LD slot prefix [0, SOFF + NS), V_i, X_i) after the per-wave scratch and filter.
+constexpr int RING_SB = 8;                       // stages per block
+constexpr int RS_SLOT = 142;                     // LD slot prefix (P | K | chol | J | 1/sc)
+constexpr int RS_V = RS_SLOT, RS_X = RS_SLOT + NBMAX;
+constexpr int RS_L = RS_SLOT + 2 * NBMAX;        // doubles per stage record
+constexpr int RING_OFF = 4 * NBMAX * NBMAX + 8 + 2 * 64;
+constexpr int RING_DOUBLES = (RING_SB + 1) * RS_L;
+
 // ---------------------------------------------------------------------------
 template <class Ctx, int EN_ = 4, int EM_ = 4, int FORM_ = 0>
 struct ObcaSolver {
@@ -317,6 +326,12 @@ struct ObcaSolver {
   // objective factor of the Hessian: sf, or 0 in the restoration phase
   HTP_HD HTP_FI double hsf() const { return rs ? 0.0 : sf; }
   long long cyc[8];
+#ifdef HTP_KKT_PROF  // experiments: KKT-solve sub-phases (local rhs sweep, stage Riccati solve, local back sweep)
+  long long kprof[3] = {0, 0, 0};
+#define HTP_KPROF(k, t) do { const long long t_ = c.clock(); kprof[k] += t_ - (t); (t) = t_; } while (0)
+#else
+#define HTP_KPROF(k, t) do { } while (0)
+#endif
 #ifdef HTP_PROF_ON  // experiments: sub-step cycle counters of the stage chain (tools/build_variants.py)
   long long pcyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   long long tprof = 0;
@@ -1156,6 +1171,12 @@ struct ObcaSolver {
     for (int k = 0; k < nrhs; ++k) bk_solve_packed(B.K, ip, NL, V + k * NL);
   }
 
+  // The three local sweeps run in two passes.  Pass 1: lane-parallel over the blocks; a block whose
+  // unpivoted LDL^T meets a non-positive multiplier pivot (B.piv: ~11 % of the blocks of config D)
+  // is only recorded, its index compacted into L.plist (ballot rank).  Pass 2: the recorded blocks,
+  // one per lane, through the Bunch-Kaufman path (local_pivoted).  Before, a 64-block trip holding
+  // any pivoted block ran that path for the whole wave -- nearly every trip.  Each block's
+  // arithmetic is unchanged, so the results are bit-identical.
   template <int EN, int EM>
   HTP_HD HTP_FI void local_factor_sweep(bool ls, double dw, double dc, int& neg, int& zero) {
     if constexpr (PT) {
@@ -1163,51 +1184,69 @@ struct ObcaSolver {
       return;
     }
     gd* PS = A(L.pairS);
-    for (int p = c.lane; p < D.P; p += c.width) {
-      LocalBlock<EN, EM> B;
-      build_local<EN, EM>(B, p, ls, dw, dc);
-      B.factor();
-      constexpr int NL = LocalBlock<EN, EM>::NL;
-      double Vp[3 * NL];
-      int bneg = B.neg, bzero = B.zero;
-      if (B.piv) {
+    gd* PL = A(L.plist);
+    constexpr int NL = LocalBlock<EN, EM>::NL;
+    auto sidx = [](int row, int col) {  // (row, col) -> xx0 xy1 yy2 xt3 yt4 tt5
+      return (col == 0) ? 0 : (col == 1 ? (row == 0 ? 1 : 2) : (row == 0 ? 3 : (row == 1 ? 4 : 5)));
+    };
+    int npiv = 0;  // wave-uniform
+    for (int b0 = 0; b0 < D.P; b0 += c.width) {
+      const int p = b0 + c.lane;
+      bool piv = false;
+      if (p < D.P) {
+        LocalBlock<EN, EM> B;
+        build_local<EN, EM>(B, p, ls, dw, dc);
+        B.factor();
+        piv = B.piv;
+        if (!piv) {
+          neg += B.neg;
+          zero |= B.zero;
+          // B' K^-1 B = W' D^-1 W with W = L^-1 B: forward substitutions only
+          double W[3][NL];
+          for (int col = 0; col < 3; ++col) {
+            for (int r = 0; r < NL; ++r) W[col][r] = B.B[r][col];
+            B.forward(W[col]);
+          }
+          double id[NL];
+          for (int r = 0; r < NL; ++r) id[r] = 1.0 / B.K[B.pk(r, r)];
+          double S[6];
+          for (int col = 0; col < 3; ++col)
+            for (int row = 0; row <= col; ++row) {
+              double acc = 0.0;
+              for (int r = 0; r < NL; ++r) acc += W[row][r] * (W[col][r] * id[r]);
+              S[sidx(row, col)] = acc;
+            }
+          for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
+        }
+      }
+      int cnt;
+      const int r = c.rank(piv, cnt);
+      if (piv) PL[npiv + r] = (double)p;
+      npiv += cnt;
+    }
+    c.sync();
+    for (int b0 = 0; b0 < npiv; b0 += c.width) {
+      const int q = b0 + c.lane;
+      if (q < npiv) {
+        const int p = (int)PL[q];
+        LocalBlock<EN, EM> B;
+        build_local<EN, EM>(B, p, ls, dw, dc);
+        double Vp[3 * NL];
         for (int col = 0; col < 3; ++col)
           for (int r = 0; r < NL; ++r) Vp[col * NL + r] = B.B[r][col];
         int pn[2];
         local_pivoted<EN, EM>(p, ls, dw, dc, Vp, 3, pn);
-        bneg = pn[0];
-        bzero = pn[1];
-      }
-      neg += bneg;
-      zero |= bzero;
-      double S[6] = {0, 0, 0, 0, 0, 0};
-      if (B.piv) {
+        neg += pn[0];
+        zero |= pn[1];
+        double S[6];
         for (int col = 0; col < 3; ++col)
           for (int row = 0; row <= col; ++row) {  // S(:,col) = B' K^-1 B(:,col)
             double acc = 0.0;
             for (int r = 0; r < NL; ++r) acc += B.B[r][row] * Vp[col * NL + r];
-            const int idx = (col == 0) ? 0 : (col == 1 ? (row == 0 ? 1 : 2) : (row == 0 ? 3 : (row == 1 ? 4 : 5)));
-            S[idx] = acc;
+            S[sidx(row, col)] = acc;
           }
-      } else {
-        // B' K^-1 B = W' D^-1 W with W = L^-1 B: forward substitutions only
-        double W[3][NL];
-        for (int col = 0; col < 3; ++col) {
-          for (int r = 0; r < NL; ++r) W[col][r] = B.B[r][col];
-          B.forward(W[col]);
-        }
-        double id[NL];
-        for (int r = 0; r < NL; ++r) id[r] = 1.0 / B.K[B.pk(r, r)];
-        for (int col = 0; col < 3; ++col)
-          for (int row = 0; row <= col; ++row) {
-            double acc = 0.0;
-            for (int r = 0; r < NL; ++r) acc += W[row][r] * (W[col][r] * id[r]);
-            // index map (row,col) -> xx0 xy1 yy2 xt3 yt4 tt5
-            const int idx = (col == 0) ? 0 : (col == 1 ? (row == 0 ? 1 : 2) : (row == 0 ? 3 : (row == 1 ? 4 : 5)));
-            S[idx] = acc;
-          }
+        for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
       }
-      for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
     }
   }
 
@@ -1220,42 +1259,67 @@ struct ObcaSolver {
       return;
     }
     gd* PR = A(L.pairR);
-    for (int p = c.lane; p < D.P; p += c.width) {
-      constexpr int NZ = LocalBlock<EN, EM>::NZ;
-      constexpr int NL = LocalBlock<EN, EM>::NL;
+    gd* PL = A(L.plist);
+    constexpr int NZ = LocalBlock<EN, EM>::NZ;
+    constexpr int NL = LocalBlock<EN, EM>::NL;
+    // block p's right-hand side v (before the solve) and the eliminated rows' q3
+    auto rhs = [&](int p, const LocalBlock<EN, EM>& B, double* v, double& q3) {
       int i, m, n, mu0, la0;
       pair_index(p, i, m, n, mu0, la0);
       const int em = D.eo[m], en = D.eb[n];
       const int re = D.ePair + 2 * p;
-      // rhs loads issue with the block's own loads (before its factorization)
       const double bd1 = bd[2 * p], bs1 = bs[2 * p], bd3 = bd[2 * p + 1], bs3 = bs[2 * p + 1];
       const double bc0 = bc[re], bc1 = bc[re + 1];
       double bxz[NZ];
       for (int j = 0; j < EN; ++j) bxz[j] = bx[mu0 + (j < en ? j : 0)];
       for (int j = 0; j < EM; ++j) bxz[EN + j] = bx[la0 + (j < em ? j : 0)];
-      LocalBlock<EN, EM> B;
-      build_local<EN, EM>(B, p, ls, dw, dc);
-      B.factor();
       const double q1 = (bd1 + bs1 / B.Ds1) / B.E1;
-      const double q3 = (bd3 + bs3 / B.Ds3) / B.E3;
-      double v[NL];
+      q3 = (bd3 + bs3 / B.Ds3) / B.E3;
       for (int j = 0; j < EN; ++j) v[j] = (j < en ? bxz[j] : 0.0) + B.J1[j] * q1 + B.J3z[j] * q3;
       for (int j = 0; j < EM; ++j) v[EN + j] = (j < em ? bxz[EN + j] : 0.0) + B.J1[EN + j] * q1 + B.J3z[EN + j] * q3;
       v[NZ] = bc0;
       v[NZ + 1] = bc1;
-      if (B.piv) {
-        double vp[NL];
-        int pn[2];
-        for (int r = 0; r < NL; ++r) vp[r] = v[r];
-        local_pivoted<EN, EM>(p, ls, dw, dc, vp, 1, pn);
-        for (int r = 0; r < NL; ++r) v[r] = vp[r];
-      } else {
-        B.solve(v);
-      }
+    };
+    auto out = [&](int p, const LocalBlock<EN, EM>& B, const double* v, double q3) {
       for (int col = 0; col < 3; ++col) {
         double acc = 0.0;
         for (int r = 0; r < NL; ++r) acc += B.B[r][col] * v[r];
         PR[3 * p + col] = -acc + (col < 2 ? B.J3p[col] * q3 : 0.0);
+      }
+    };
+    int npiv = 0;
+    for (int b0 = 0; b0 < D.P; b0 += c.width) {
+      const int p = b0 + c.lane;
+      bool piv = false;
+      if (p < D.P) {
+        LocalBlock<EN, EM> B;
+        build_local<EN, EM>(B, p, ls, dw, dc);
+        B.factor();
+        piv = B.piv;
+        if (!piv) {
+          double v[NL], q3;
+          rhs(p, B, v, q3);
+          B.solve(v);
+          out(p, B, v, q3);
+        }
+      }
+      int cnt;
+      const int r = c.rank(piv, cnt);
+      if (piv) PL[npiv + r] = (double)p;
+      npiv += cnt;
+    }
+    c.sync();
+    for (int b0 = 0; b0 < npiv; b0 += c.width) {
+      const int q = b0 + c.lane;
+      if (q < npiv) {
+        const int p = (int)PL[q];
+        LocalBlock<EN, EM> B;
+        build_local<EN, EM>(B, p, ls, dw, dc);
+        double v[NL], q3;
+        rhs(p, B, v, q3);
+        int pn[2];
+        local_pivoted<EN, EM>(p, ls, dw, dc, v, 1, pn);
+        out(p, B, v, q3);
       }
     }
   }
@@ -1268,40 +1332,37 @@ struct ObcaSolver {
       local_back_sweep_pt(ls, dw, dc, bx, bs, bd, ox, os, od);
       return;
     }
-    for (int p = c.lane; p < D.P; p += c.width) {
-      constexpr int NZ = LocalBlock<EN, EM>::NZ;
-      constexpr int NL = LocalBlock<EN, EM>::NL;
+    gd* PL = A(L.plist);
+    constexpr int NZ = LocalBlock<EN, EM>::NZ;
+    constexpr int NL = LocalBlock<EN, EM>::NL;
+    // block p's right-hand side minus its coupling to the stage step dp = (dx, dy, dtheta), before the solve
+    auto rhs = [&](int p, const LocalBlock<EN, EM>& B, double* v, double& dpx, double& dpy) {
       int i, m, n, mu0, la0;
       pair_index(p, i, m, n, mu0, la0);
       const int em = D.eo[m], en = D.eb[n];
       const int re = D.ePair + 2 * p;
-      // rhs loads issue with the block's own loads (before its factorization)
       const double bd1 = bd[2 * p], bs1 = bs[2 * p], bd3 = bd[2 * p + 1], bs3 = bs[2 * p + 1];
       const double bc0 = bc[re], bc1 = bc[re + 1];
-      const double dpx = ox[NS * i], dpy = ox[NS * i + 1], dth = ox[NS * i + 3];
+      dpx = ox[NS * i];
+      dpy = ox[NS * i + 1];
+      const double dth = ox[NS * i + 3];
       double bxz[NZ];
       for (int j = 0; j < EN; ++j) bxz[j] = bx[mu0 + (j < en ? j : 0)];
       for (int j = 0; j < EM; ++j) bxz[EN + j] = bx[la0 + (j < em ? j : 0)];
-      LocalBlock<EN, EM> B;
-      build_local<EN, EM>(B, p, ls, dw, dc);
-      B.factor();
       const double q1 = (bd1 + bs1 / B.Ds1) / B.E1;
       const double q3 = (bd3 + bs3 / B.Ds3) / B.E3;
-      double v[NL];
       for (int j = 0; j < EN; ++j) v[j] = (j < en ? bxz[j] : 0.0) + B.J1[j] * q1 + B.J3z[j] * q3;
       for (int j = 0; j < EM; ++j) v[EN + j] = (j < em ? bxz[EN + j] : 0.0) + B.J1[EN + j] * q1 + B.J3z[EN + j] * q3;
       v[NZ] = bc0;
       v[NZ + 1] = bc1;
       for (int r = 0; r < NL; ++r) v[r] -= B.B[r][0] * dpx + B.B[r][1] * dpy + B.B[r][2] * dth;
-      if (B.piv) {
-        double vp[NL];
-        int pn[2];
-        for (int r = 0; r < NL; ++r) vp[r] = v[r];
-        local_pivoted<EN, EM>(p, ls, dw, dc, vp, 1, pn);
-        for (int r = 0; r < NL; ++r) v[r] = vp[r];
-      } else {
-        B.solve(v);
-      }
+    };
+    auto out = [&](int p, const LocalBlock<EN, EM>& B, const double* v, double dpx, double dpy) {
+      int i, m, n, mu0, la0;
+      pair_index(p, i, m, n, mu0, la0);
+      const int em = D.eo[m], en = D.eb[n];
+      const int re = D.ePair + 2 * p;
+      const double bd1 = bd[2 * p], bs1 = bs[2 * p], bd3 = bd[2 * p + 1], bs3 = bs[2 * p + 1];
       for (int j = 0; j < en; ++j) ox[mu0 + j] = v[j];
       for (int j = 0; j < em; ++j) ox[la0 + j] = v[EN + j];
       oc[re] = v[NZ];
@@ -1317,6 +1378,41 @@ struct ObcaSolver {
       od[2 * p + 1] = y3;
       os[2 * p] = (bs1 + y1) / B.Ds1;
       os[2 * p + 1] = (bs3 + y3) / B.Ds3;
+    };
+    int npiv = 0;
+    for (int b0 = 0; b0 < D.P; b0 += c.width) {
+      const int p = b0 + c.lane;
+      bool piv = false;
+      if (p < D.P) {
+        LocalBlock<EN, EM> B;
+        build_local<EN, EM>(B, p, ls, dw, dc);
+        B.factor();
+        piv = B.piv;
+        if (!piv) {
+          double v[NL], dpx, dpy;
+          rhs(p, B, v, dpx, dpy);
+          B.solve(v);
+          out(p, B, v, dpx, dpy);
+        }
+      }
+      int cnt;
+      const int r = c.rank(piv, cnt);
+      if (piv) PL[npiv + r] = (double)p;
+      npiv += cnt;
+    }
+    c.sync();
+    for (int b0 = 0; b0 < npiv; b0 += c.width) {
+      const int q = b0 + c.lane;
+      if (q < npiv) {
+        const int p = (int)PL[q];
+        LocalBlock<EN, EM> B;
+        build_local<EN, EM>(B, p, ls, dw, dc);
+        double v[NL], dpx, dpy;
+        rhs(p, B, v, dpx, dpy);
+        int pn[2];
+        local_pivoted<EN, EM>(p, ls, dw, dc, v, 1, pn);
+        out(p, B, v, dpx, dpy);
+      }
     }
   }
 
@@ -2291,21 +2387,55 @@ struct ObcaSolver {
     return bad;
   }
 
-  // V (block order [y|x|u|tau]) -> X (same order), the two passes on the matrix core
+  // V (block order [y|x|u|tau]) -> X (same order), the two passes on the matrix core.
+  // Stage data reach the passes through an LDS ring of RING_SB + 1 stage records (the LD slot's
+  // P | K | chol(Rt) | J | 1/sc prefix, V_i, X_i): one cooperative, coalesced global -> LDS copy
+  // per block of RING_SB stages, so a block pays one memory latency instead of one per stage;
+  // the MFMA operands of stage i are then gathered from LDS one stage ahead (values unchanged:
+  // bit-identical to gathering them from HBM).
+  // stages [lo, lo + cnt) of LD / V / X into the ring (cnt <= RING_SB + 1); stages >= N skipped
+  HTP_HD HTP_FI void ring_fill(ld* ring, int lo, int cnt, const gd* V, const gd* X) {
+    const int N = D.N, nb = D.nb;
+    const int64_t nb2 = (int64_t)nb * nb;
+    const gd* LDa = A(L.LD);
+    const int tot = cnt * RS_L;
+    constexpr int U = ((RING_SB + 1) * RS_L + 63) / 64;
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {                       // every load of the block issues first
+      const int e = c.lane + u * c.width, sidx = e / RS_L, k = e - sidx * RS_L, st = lo + sidx;
+      const bool ok = e < tot && st < N;
+      const int stc = ok ? st : 0;
+      const gd* src = k < RS_SLOT ? LDa + (int64_t)stc * nb2 + k
+                    : (k < RS_X ? V + (int64_t)stc * nb + (k - RS_V) : X + (int64_t)stc * nb + (k - RS_X));
+      const bool in_blk = k < RS_SLOT || (k < RS_X ? k - RS_V < nb : k - RS_X < nb);
+      v[u] = (ok && in_blk) ? *src : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = c.lane + u * c.width;
+      if (e < tot) ring[e] = v[u];
+    }
+  }
+
   HTP_HD HTP_FI void riccati_solve_mfma(const gd* V, gd* X) {
     const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
-    const int64_t nb2 = (int64_t)nb * nb;
     const int col = c.lane & 15, rg = c.lane >> 4;
     const bool c0 = col == 0;
-    const gd* LDa = A(L.LD);
+    ld* ring = c.lds + RING_OFF;
     // per-lane record maps: F rows as B / F' as A (2), F as A (3), P as A (2), K' as A (1), K at rows V0.. as A (2)
     FSrc fT[2], fA[3];
     for (int sgm = 0; sgm < 2; ++sgm) fT[sgm] = f_src(rg + 4 * sgm, col);
     for (int sgm = 0; sgm < 3; ++sgm) fA[sgm] = f_src(col, rg + 4 * sgm);
-    auto p_at = [&](const gd* slot, int sgm) {  // P[col][4 sgm + rg] (P symmetric, 8 x 8 stride 8)
+    auto p_at = [&](const ld* slot, int sgm) {  // P[col][4 sgm + rg] (P symmetric, 8 x 8 stride 8)
       const int k = rg + 4 * sgm;
-      return (col < nz && k < nz) ? slot[col * 8 + k] : 0.0;
+      return (col < nz && k < nz) ? (double)slot[col * 8 + k] : 0.0;
     };
+    auto f_at = [&](const FSrc& f, const ld* slot) {
+      return f.kind == 3 ? (double)slot[f.off] : (f.kind == 4 ? 1.0 : 0.0);
+    };
+    int lo = 0;                                       // first stage held by the ring
+    auto rs = [&](int i) -> const ld* { return ring + (i - lo) * RS_L; };
     // ---------------- backward
     // p_{N-1} = [q_{N-1}; 0]
     dbl4 pv = {0.0, 0.0, 0.0, 0.0};
@@ -2324,40 +2454,46 @@ struct ObcaSolver {
     // e_{i+1} (B, 2, unscaled)
     struct BRec { double mp[2], ft[2], kt, qr[3], e[2]; };
     auto ld_b = [&](int i, BRec& R) {
-      const gd* slot = LDa + (int64_t)i * nb2;
-      const gd* nslot = slot + nb2;
+      const ld* slot = rs(i);
+      const ld* nslot = slot + RS_L;
       for (int sgm = 0; sgm < 2; ++sgm) {
         R.mp[sgm] = -p_at(nslot, sgm);
-        R.ft[sgm] = f_get(fT[sgm], slot);
+        R.ft[sgm] = f_at(fT[sgm], slot);
         const int row = rg + 4 * sgm;
-        R.e[sgm] = (c0 && row < NS) ? V[(int64_t)(i + 1) * nb + row] * nslot[SOFF + row] : 0.0;
+        R.e[sgm] = (c0 && row < NS) ? nslot[RS_V + row] * nslot[SOFF + row] : 0.0;
       }
-      R.kt = (rg < nv && col < nz) ? slot[64 + rg * 8 + col] : 0.0;
+      R.kt = (rg < nv && col < nz) ? (double)slot[64 + rg * 8 + col] : 0.0;
       for (int r = 0; r < 3; ++r) {
         const int row = rg + 4 * r;
         double v = 0.0;
-        if (c0 && row < NS) v = V[(int64_t)i * nb + NS + row];
-        else if (c0 && row >= V0 && row < V0 + nv) v = V[(int64_t)i * nb + NS + NS + (row - V0)];
+        if (c0 && row < NS) v = slot[RS_V + NS + row];
+        else if (c0 && row >= V0 && row < V0 + nv) v = slot[RS_V + NS + NS + (row - V0)];
         R.qr[r] = v;
       }
     };
     BRec bc, bn;
-    if (N >= 2) ld_b(N - 2, bc);
-    for (int i = N - 2; i >= 0; --i) {
-      if (i > 0) ld_b(i - 1, bn);
-      dbl4 w = Ctx::mfma16(bc.mp[0], bc.e[0], pv);          // w = p - P e
-      w = Ctx::mfma16(bc.mp[1], bc.e[1], w);
-      dbl4 g = {bc.qr[0], bc.qr[1], bc.qr[2], 0.0};         // g = [q; r] + F' w
-      g = Ctx::mfma16(bc.ft[0], w[0], g);
-      g = Ctx::mfma16(bc.ft[1], w[1], g);
-      pv = Ctx::mfma16(bc.kt, g[2], g);                      // p = g_z + K' rt   (rt = g rows V0..)
-      gd* Xi = X + (int64_t)i * nb;
-      for (int r = 0; r < 2; ++r) {
-        const int row = rg + 4 * r;
-        if (c0 && row < nz) Xi[row] = pv[r];
+    for (int hi = N - 2; hi >= 0; hi -= RING_SB) {
+      lo = hi - RING_SB + 1 > 0 ? hi - RING_SB + 1 : 0;
+      c.sync();                                       // the previous block's LDS reads are done
+      ring_fill(ring, lo, hi - lo + 2, V, X);         // stages lo .. hi + 1
+      c.sync();
+      ld_b(hi, bc);
+      for (int i = hi; i >= lo; --i) {
+        if (i > lo) ld_b(i - 1, bn);
+        dbl4 w = Ctx::mfma16(bc.mp[0], bc.e[0], pv);          // w = p - P e
+        w = Ctx::mfma16(bc.mp[1], bc.e[1], w);
+        dbl4 g = {bc.qr[0], bc.qr[1], bc.qr[2], 0.0};         // g = [q; r] + F' w
+        g = Ctx::mfma16(bc.ft[0], w[0], g);
+        g = Ctx::mfma16(bc.ft[1], w[1], g);
+        pv = Ctx::mfma16(bc.kt, g[2], g);                      // p = g_z + K' rt   (rt = g rows V0..)
+        gd* Xi = X + (int64_t)i * nb;
+        for (int r = 0; r < 2; ++r) {
+          const int row = rg + 4 * r;
+          if (c0 && row < nz) Xi[row] = pv[r];
+        }
+        if (c0 && rg < nv) Xi[nz + rg] = g[2];
+        bc = bn;
       }
-      if (c0 && rg < nv) Xi[nz + rg] = g[2];
-      bc = bn;
     }
     c.sync();
     HTP_PROF(6);
@@ -2372,52 +2508,58 @@ struct ObcaSolver {
     // e_{i+1} (C, 2), rt_i (3) + chol(Rt_i) (9), 1/sc of y_i (2)
     struct FRec { double mp[2], p[2], ka[2], fa[3], e[2], rt[3], lc[9], isc[2]; };
     auto ld_f = [&](int i, FRec& R) {
-      const gd* slot = LDa + (int64_t)i * nb2;
-      const gd* Xi = X + (int64_t)i * nb;
+      const ld* slot = rs(i);
+      const ld* nslot = slot + RS_L;
       const bool last = i >= N - 1;
       for (int sgm = 0; sgm < 2; ++sgm) {
         const int row = rg + 4 * sgm, k = rg + 4 * sgm;
         R.mp[sgm] = -p_at(slot, sgm);
-        R.p[sgm] = (c0 && row < nz) ? Xi[row] : 0.0;
-        R.ka[sgm] = (!last && col >= V0 && col < V0 + nv && k < nz) ? slot[64 + (col - V0) * 8 + k] : 0.0;
-        R.e[sgm] = (!last && c0 && row < NS) ? V[(int64_t)(i + 1) * nb + row] * slot[nb2 + SOFF + row] : 0.0;
-        R.isc[sgm] = (row < NS) ? slot[SOFF + row] : 0.0;
+        R.p[sgm] = (c0 && row < nz) ? (double)slot[RS_X + row] : 0.0;
+        R.ka[sgm] = (!last && col >= V0 && col < V0 + nv && k < nz) ? (double)slot[64 + (col - V0) * 8 + k] : 0.0;
+        R.e[sgm] = (!last && c0 && row < NS) ? nslot[RS_V + row] * nslot[SOFF + row] : 0.0;
+        R.isc[sgm] = (row < NS) ? (double)slot[SOFF + row] : 0.0;
       }
-      for (int sgm = 0; sgm < 3; ++sgm) R.fa[sgm] = last ? 0.0 : f_get(fA[sgm], slot);
-      for (int a = 0; a < 3; ++a) R.rt[a] = (!last && a < nv) ? Xi[nz + a] : 0.0;
-      for (int k = 0; k < 9; ++k) R.lc[k] = last ? 0.0 : slot[88 + k];
+      for (int sgm = 0; sgm < 3; ++sgm) R.fa[sgm] = last ? 0.0 : f_at(fA[sgm], slot);
+      for (int a = 0; a < 3; ++a) R.rt[a] = (!last && a < nv) ? (double)slot[RS_X + nz + a] : 0.0;
+      for (int k = 0; k < 9; ++k) R.lc[k] = last ? 0.0 : (double)slot[88 + k];
     };
     FRec fc, fn;
-    ld_f(0, fc);
-    for (int i = 0; i < N; ++i) {
-      if (i + 1 < N) ld_f(i + 1, fn);
-      dbl4 y = {fc.p[0], fc.p[1], 0.0, 0.0};                 // y = p - P z
-      y = Ctx::mfma16(fc.mp[0], zu[0], y);
-      y = Ctx::mfma16(fc.mp[1], zu[1], y);
-      gd* Xi = X + (int64_t)i * nb;
-      const double zr0 = zu[0], zr1 = zu[1];
-      for (int r = 0; r < 2; ++r) {
-        const int row = rg + 4 * r;
-        if (c0 && row < NS) Xi[row] = y[r] * fc.isc[r];
+    for (lo = 0; lo < N; lo += RING_SB) {
+      const int hi = lo + RING_SB - 1 < N - 1 ? lo + RING_SB - 1 : N - 1;
+      c.sync();
+      ring_fill(ring, lo, hi - lo + 2, V, X);         // stages lo .. hi + 1 (X_i holds p_i, rt_i here)
+      c.sync();
+      ld_f(lo, fc);
+      for (int i = lo; i <= hi; ++i) {
+        if (i < hi) ld_f(i + 1, fn);
+        dbl4 y = {fc.p[0], fc.p[1], 0.0, 0.0};                 // y = p - P z
+        y = Ctx::mfma16(fc.mp[0], zu[0], y);
+        y = Ctx::mfma16(fc.mp[1], zu[1], y);
+        gd* Xi = X + (int64_t)i * nb;
+        const double zr0 = zu[0], zr1 = zu[1];
+        for (int r = 0; r < 2; ++r) {
+          const int row = rg + 4 * r;
+          if (c0 && row < NS) Xi[row] = y[r] * fc.isc[r];
+        }
+        if (i < N - 1) {
+          double kv[3] = {fc.rt[0], fc.rt[1], fc.rt[2]};
+          chol3_solve(fc.lc, nv, kv);
+          dbl4 u = {zu[0], zu[1], (c0 && rg < nv) ? kv[rg] : 0.0, 0.0};  // u = [z; Rt^-1 rt + K z]
+          u = Ctx::mfma16(fc.ka[0], zu[0], u);
+          u = Ctx::mfma16(fc.ka[1], zu[1], u);
+          if (c0 && rg < nv) Xi[NS + NS + rg] = u[2];
+          dbl4 zn = {fc.e[0], fc.e[1], 0.0, 0.0};              // z_{i+1} = F u + e
+          zn = Ctx::mfma16(fc.fa[0], u[0], zn);
+          zn = Ctx::mfma16(fc.fa[1], u[1], zn);
+          zn = Ctx::mfma16(fc.fa[2], u[2], zn);
+          zu = zn;
+        }
+        for (int r = 0; r < 2; ++r) {
+          const int row = rg + 4 * r;
+          if (c0 && row < NS) Xi[NS + row] = r == 0 ? zr0 : zr1;
+        }
+        fc = fn;
       }
-      if (i < N - 1) {
-        double kv[3] = {fc.rt[0], fc.rt[1], fc.rt[2]};
-        chol3_solve(fc.lc, nv, kv);
-        dbl4 u = {zu[0], zu[1], (c0 && rg < nv) ? kv[rg] : 0.0, 0.0};  // u = [z; Rt^-1 rt + K z]
-        u = Ctx::mfma16(fc.ka[0], zu[0], u);
-        u = Ctx::mfma16(fc.ka[1], zu[1], u);
-        if (c0 && rg < nv) Xi[NS + NS + rg] = u[2];
-        dbl4 zn = {fc.e[0], fc.e[1], 0.0, 0.0};              // z_{i+1} = F u + e
-        zn = Ctx::mfma16(fc.fa[0], u[0], zn);
-        zn = Ctx::mfma16(fc.fa[1], u[1], zn);
-        zn = Ctx::mfma16(fc.fa[2], u[2], zn);
-        zu = zn;
-      }
-      for (int r = 0; r < 2; ++r) {
-        const int row = rg + 4 * r;
-        if (c0 && row < NS) Xi[NS + row] = r == 0 ? zr0 : zr1;
-      }
-      fc = fn;
     }
     c.sync();
     HTP_PROF(7);
@@ -2784,8 +2926,12 @@ struct ObcaSolver {
       bc = fc;
       bd = fd;
     }
+#ifdef HTP_KKT_PROF
+    long long tk = c.clock();
+#endif
     local_rhs_sweep<EN_, EM_>(ls, dw, dc, bx, bs, bc, bd);
     c.sync();
+    HTP_KPROF(0, tk);
     const gd* PR = A(L.pairR);
     const gd* scE = A(L.scE);
     gd* V = A(L.V);
@@ -2889,8 +3035,10 @@ struct ObcaSolver {
       }
     }
     c.sync();
+    HTP_KPROF(1, tk);
     local_back_sweep<EN_, EM_>(ls, dw, dc, bx, bs, bc, bd, ox, os, oc, od);
     c.sync();
+    HTP_KPROF(2, tk);
     if (rs) {  // dn = (b_n - dy) / (S_n + dw), dp = (b_p + dy) / (S_p + dw)
       for (int r = c.lane; r < D.mc + D.md; r += c.width) {
         const int j = r < D.mc ? r : r + D.mc, jp = r < D.mc ? r + D.mc : r + D.mc + D.md;
@@ -3456,6 +3604,9 @@ struct ObcaSolver {
 #ifdef HTP_PROF_ON
       for (int k = 0; k < 8; ++k)
         if (k != 4) res.cyc[k] = pcyc[k];
+#endif
+#ifdef HTP_KKT_PROF
+      for (int k = 0; k < 3; ++k) res.cyc[5 + k] = kprof[k];
 #endif
       res.cyc[4] = c.clock() - t0;
     }

@@ -55,6 +55,14 @@ struct ThreadWave {
     sync();
     return s;
   }
+  int rank(bool pred, int& total) const {
+    sync(); sh->ired[lane] = pred ? 1 : 0; sync();
+    int r = 0, t = 0;
+    for (int i = 0; i < 64; ++i) { if (i < lane) r += sh->ired[i]; t += sh->ired[i]; }
+    sync();
+    total = t;
+    return r;
+  }
   long long clock() const { return 0; }
   long long wall() const { return 0; }
   double uniform(double v) const { return v; }

@@ -57,6 +57,12 @@ struct DevWave {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return __builtin_amdgcn_readfirstlane(v);
   }
+  // compaction: this lane's index among the lanes with `pred` set, and (uniform) how many are set
+  __device__ __forceinline__ int rank(bool pred, int& total) const {
+    const unsigned long long m = __ballot(pred ? 1 : 0);
+    total = __builtin_amdgcn_readfirstlane((int)__popcll(m));
+    return (int)__popcll(m & ((1ull << lane) - 1ull));
+  }
   __device__ __forceinline__ double uniform(double v) const { return uni(v); }
   __device__ __forceinline__ int uniform_i(int v) const { return __builtin_amdgcn_readfirstlane(v); }
   __device__ __forceinline__ double bcast(double v, int src) const { return __shfl(v, src, 64); }
@@ -87,6 +93,7 @@ struct HostLane {
   double maxv(double v) const { return v; }
   double minv(double v) const { return v; }
   int isum(int v) const { return v; }
+  int rank(bool pred, int& total) const { total = pred ? 1 : 0; return 0; }
   double bcast(double v, int) const { return v; }
   double uniform(double v) const { return v; }
   int uniform_i(int v) const { return v; }

@@ -1,0 +1,41 @@
+"""A/B of libhtp_<name>.so variants on one config batch (experiments only):
+kernel time, solves/s, bit-identity against the first variant, and the
+per-phase cycle shares; variants built with -DHTP_KKT_PROF report the KKT
+solve's sub-phases (local rhs sweep, stage Riccati solve, local back sweep) in
+the last three slots.   python tools/ab_phase.py CFG B name1 name2 ..."""
+import sys
+
+import numpy as np
+
+sys.path.insert(0, ".")
+from headland_trajectory_planning_amd import _native  # noqa: E402
+import bench  # noqa: E402
+
+cfg, B = sys.argv[1], int(sys.argv[2])
+names = sys.argv[3:]
+pk = _native.PackedBatch(bench.make_batch(list(range(B)), cfg, 16))
+ctxs = {}
+for n in names:
+    path = _native.LIB_PATH if n == "base" else _native.LIB_PATH.replace("libhtp.so", f"libhtp_{n}.so")
+    ctxs[n] = _native.Context(0, lib=_native.load(path))
+ref = None
+for rnd in range(2):
+    for k, ctx in ctxs.items():
+        r = ctx.solve(pk)
+        ms = ctx.last_kernel_ms()
+        ok = ""
+        if ref is None:
+            ref = r
+        else:
+            ok = f" max|dx|={np.max(np.abs(ref.x - r.x)):.2e} status_eq={np.array_equal(ref.status, r.status)} " \
+                 f"iters_eq={np.array_equal(ref.iterations, r.iterations)}"
+        line = f"round {rnd} {k}: kernel {ms:.1f} ms {B / (ms / 1e3):.0f} solves/s iters {r.iterations.mean():.2f}{ok}"
+        if rnd == 1:
+            cyc = ctx.last_cycles(B).astype(float)
+            tot = cyc[:, 4].sum()
+            tail = ["rhs_sweep", "ric_solve", "back_sweep"] if "kprof" in k else ["errors", "linesearch", "update"]
+            head = ["build", "ldlt", "schur"] if "lprof" in k else ["local", "assemble", "chain"]
+            nm = head + ["kktsolve", "total"] + tail
+            line += " | " + " ".join(f"{nm[j]} {cyc[:, j].sum() / tot:.3f}" for j in (0, 1, 2, 3, 5, 6, 7))
+            line += " | per-iter cycles %.3g" % (cyc[:, 4] / np.maximum(1, r.iterations)).mean()
+        print(line, flush=True)
