@@ -265,14 +265,14 @@ def main():
     # HBM bytes per problem-iteration measured with rocprofv3 FETCH_SIZE/WRITE_SIZE
     # passes (tools/gpu_pmc.sh -> profiles/*_traffic.json) for this workload, scaled
     # to the same iteration count as `achieved`.
-    tf = os.environ.get("HTP_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r02_traffic.json"))
+    tf = os.environ.get("HTP_TRAFFIC_JSON", os.path.join(ROOT, "profiles", f"r02_traffic_{args.config}.json"))
     if tf and os.path.exists(tf):
         tj = json.load(open(tf))
         if tj.get("workload") == args.config and tj.get("bytes_per_problem_iter") \
                 and tj.get("solver_sha") == _native.core_sha():
             traffic = tj["bytes_per_problem_iter"] * it_sum / (kernel_ms * 1e-3) / 1e9
     mfma = None
-    mf = os.environ.get("HTP_MFMA_JSON", os.path.join(ROOT, "profiles", "r02_mfma.json"))
+    mf = os.environ.get("HTP_MFMA_JSON", os.path.join(ROOT, "profiles", f"r02_mfma_{args.config}.json"))
     if mf and os.path.exists(mf):
         mj = json.load(open(mf))
         if mj.get("solver_sha") == _native.core_sha():

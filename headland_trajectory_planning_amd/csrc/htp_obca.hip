@@ -21,7 +21,7 @@ using namespace htp;
 
 namespace {
 
-constexpr int LDS_D = RING_OFF + RING_DOUBLES;  // scratch + filter (obca_core.h) + Riccati stage ring
+constexpr int LDS_D = LDS_WAVE_DOUBLES;  // scratch + filter + Riccati stage ring / pivoted blocks (obca_core.h)
 
 #ifndef HTP_WAVES_PER_EU
 #define HTP_WAVES_PER_EU 1

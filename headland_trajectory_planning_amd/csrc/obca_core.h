@@ -186,10 +186,12 @@ struct PtBlock {
 // Bunch-Kaufman LDL^T (LAPACK dsytf2 / dsytrs, lower) of a packed symmetric
 // n x n matrix, for the rare local blocks that need interchanges.  Run-time
 // indexing: these live in their own (not inlined) frame.
-HTP_HD inline double& pk_at(double* K, int r, int c) { return r >= c ? K[r * (r + 1) / 2 + c] : K[c * (c + 1) / 2 + r]; }
-HTP_HD inline double pk_at(const double* K, int r, int c) { return r >= c ? K[r * (r + 1) / 2 + c] : K[c * (c + 1) / 2 + r]; }
+// T = double (private memory) or an LDS double (device: the pivoted blocks' lane-private LDS slice)
+template <class T>
+HTP_HD inline T& pk_at(T* K, int r, int c) { return r >= c ? K[r * (r + 1) / 2 + c] : K[c * (c + 1) / 2 + r]; }
 
-HTP_HD inline void bk_factor_packed(double* K, int* ip, int n, int& neg, int& zero) {
+template <class T>
+HTP_HD inline void bk_factor_packed(T* K, int* ip, int n, int& neg, int& zero) {
   const double alpha = 0.6403882032022076;
   neg = 0;
   zero = 0;
@@ -247,7 +249,8 @@ HTP_HD inline void bk_factor_packed(double* K, int* ip, int n, int& neg, int& ze
   }
 }
 
-HTP_HD inline void bk_solve_packed(const double* K, const int* ip, int n, double* v) {
+template <class T>
+HTP_HD inline void bk_solve_packed(T* K, const int* ip, int n, double* v) {
   int k = 0;
   while (k < n) {
     if (ip[k] >= 0) {
@@ -295,6 +298,10 @@ constexpr int RS_V = RS_SLOT, RS_X = RS_SLOT + NBMAX;
 constexpr int RS_L = RS_SLOT + 2 * NBMAX;        // doubles per stage record
 constexpr int RING_OFF = 4 * NBMAX * NBMAX + 8 + 2 * 64;
 constexpr int RING_DOUBLES = (RING_SB + 1) * RS_L;
+// pivoted local blocks (ObcaSolver::local_pivoted) on the device: one packed 10x10 block per lane in LDS,
+// over the same region as the ring (never live at the same time)
+constexpr int PIV_LDS_PER_LANE = 55;
+constexpr int LDS_WAVE_DOUBLES = RING_OFF + (RING_DOUBLES > 64 * PIV_LDS_PER_LANE ? RING_DOUBLES : 64 * PIV_LDS_PER_LANE);
 
 // ---------------------------------------------------------------------------
 template <class Ctx, int EN_ = 4, int EM_ = 4, int FORM_ = 0>
@@ -1164,9 +1171,22 @@ struct ObcaSolver {
   __attribute__((noinline)) HTP_HD void local_pivoted(int p, bool ls, double dw, double dc, double* V, int nrhs,
                                                       int* inertia) const {
     constexpr int NL = LocalBlock<EN, EM>::NL;
+    constexpr int NPK = LocalBlock<EN, EM>::NPK;
     LocalBlock<EN, EM> B;
     build_local<EN, EM>(B, p, ls, dw, dc);
     int ip[NL];
+#if defined(__HIPCC__)
+    // Device, 4-edge blocks: dsytf2 on this lane's LDS slice instead of a runtime-indexed private
+    // array (every update a scratch read-modify-write).  Free here: the slice overlaps only the
+    // Riccati ring, which no local sweep uses.  Same arithmetic, bit-identical.
+    if constexpr (Ctx::kMfma && NPK <= PIV_LDS_PER_LANE) {
+      ld* K = c.lds + RING_OFF + c.lane * NPK;
+      for (int q = 0; q < NPK; ++q) K[q] = B.K[q];
+      bk_factor_packed(K, ip, NL, inertia[0], inertia[1]);
+      for (int k = 0; k < nrhs; ++k) bk_solve_packed(K, ip, NL, V + k * NL);
+      return;
+    }
+#endif
     bk_factor_packed(B.K, ip, NL, inertia[0], inertia[1]);
     for (int k = 0; k < nrhs; ++k) bk_solve_packed(B.K, ip, NL, V + k * NL);
   }

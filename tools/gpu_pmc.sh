@@ -12,7 +12,7 @@ ARGS=${*:---batch 4096}
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 pass() {  # name, counters
-  timeout -s KILL 300 rocprofv3 --pmc $2 --output-format csv -d gpurun_out/${TAG}_pmc_$1 -o $1 -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > gpurun_out/${TAG}_pmc_$1.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc $2 --output-format csv -d gpurun_out/${TAG}_pmc_$1 -o $1 -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --gen-procs 1 $ARGS > gpurun_out/${TAG}_pmc_$1.log 2>&1
   rc=$?; echo "$1 rc=$rc"; return $rc
 }
 pass fetch FETCH_SIZE || exit 1

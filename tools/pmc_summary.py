@@ -94,7 +94,7 @@ def main():
             mf["kernel_ms"] = smeta["ns"] * 1e-6
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     for name, obj in (("traffic", traffic), ("mfma", mf)):
-        path = os.path.join(ROOT, "profiles", f"{out_tag}_{name}.json")
+        path = os.path.join(ROOT, "profiles", f"{out_tag}_{name}_{cfg}.json")
         json.dump(obj, open(path, "w"), indent=1)
         print(path, json.dumps(obj)[:600])
 
