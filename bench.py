@@ -13,7 +13,10 @@ Execution: each rank runs ONE persistent launch (as many wavefronts as the GPU
 holds at once) for all K timed steps; its waves claim problem tickets from a
 host work queue (libhtp htp_queue_*), so a slow solve holds one wavefront, never
 the launch, and step k+1's problems fill the chip while step k's last solves
-finish.  Multi-GPU: one process per GPU (torch.distributed.run); the K steps'
+finish.  The default of 6 timed steps measures the sustained rate: with a
+persistent launch only the last step's slowest solves form a tail (a few
+restoration-phase problems run >1000 IPM iterations), and 3 steps leave ~15 %
+of the run in that tail (DESIGN.md s.5 gives both).  Multi-GPU: one process per GPU (torch.distributed.run); the K steps'
 tickets are cut into chunks, every rank starts on its contiguous share and, once
 that is empty, steals tail chunks of the busiest rank (scheduler.py: one
 all-gather of next-chunk counters per round).  The timed region is bracketed by
@@ -137,7 +140,7 @@ def cpu_baseline(pk, budget_s=20.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="D")
     ap.add_argument("--batch", type=int, default=0,
