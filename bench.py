@@ -150,6 +150,10 @@ def main():
     ap.add_argument("--gen-procs", type=int, default=16, help="CPU worker processes for instance generation")
     ap.add_argument("--chunk", type=int, default=256,
                     help="problems per work-stealing chunk (multi-GPU)")
+    ap.add_argument("--max-cpu-time", type=float, default=20.0,
+                    help="per-problem time limit in seconds (device wall clock), as the reference's "
+                         "OBCAOptimizer.solve(max_cpu_time=20) passes to IPOPT (R/obca_py/optimizer.py:475,486); "
+                         "0 = off")
     ap.add_argument("--waves", type=int, default=0,
                     help="wavefronts of the persistent launch (default: as many as are resident at once)")
     args = ap.parse_args()
@@ -178,6 +182,7 @@ def main():
     dev_in = {k: torch.from_numpy(getattr(pk, k)).to(dev) for k in pk.INPUTS if getattr(pk, k) is not None}
     ptrs = {k: v.data_ptr() for k, v in dev_in.items()}
     ctx = _native.Context(local)
+    ctx.set_option("max_cpu_time", args.max_cpu_time)
     stream = torch.cuda.Stream(dev)
     x_out = torch.empty((GB, pk.n_var), dtype=torch.float64, device=dev)
     waves = args.waves or ctx.resident_waves(pk)
@@ -289,7 +294,7 @@ def main():
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (Philox-seeded orchard headlands, synth.py)",
         "config": {"workload": f"config {args.config}: global batch {GB} split over {world} GPU(s), "
                                f"N={N} horizon, M={M} obstacles, K={pk.K} bodies ({imp}), time-opt on; "
-                               f"IPOPT-restated IPM to tol 1e-8",
+                               f"IPOPT-restated IPM to tol 1e-8, max_cpu_time {args.max_cpu_time:g} s per problem",
                    "global_batch": GB, "N": N, "M": M, "K": pk.K, "turn_types": synth.TURNS[args.config],
                    "turn_histogram_rank0_slice": getattr(pk, "turns", None),
                    "parallelism": f"problem-sharded x{world}, work stealing"},
@@ -297,6 +302,7 @@ def main():
                       "chunk": args.chunk if world > 1 else GB * args.steps, "chunks_rank0": len(loop.solved),
                       "stolen_chunks_total": n_solved[2], "rounds_rank0": loop.rounds, "gen_s": gen_s},
         "solver": {"success_rate": all_ok / total_solves, "mean_iters": all_iters / total_solves,
+                   "status_counts_rank0": {str(k): int(v) for k, v in zip(*np.unique(timed_st, return_counts=True))},
                    "restorations_rank0": int(timed_nr[mine].sum()),
                    "p99_iters_rank0": float(np.percentile(timed_it[mine], 99)) if mine.any() else None,
                    "max_iters_rank0": int(timed_it[mine].max()) if mine.any() else None},
