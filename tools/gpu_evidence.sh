@@ -1,0 +1,43 @@
+#!/bin/bash
+# GPU evidence runs (through gpurun, from the repo root; libraries prebuilt in-tree).
+#   tools/gpu_evidence.sh TAG STEP...      STEP in:
+#     tests    pytest -m gpu + smoke()
+#     bench    default bench line (config D 32768, 6 steps, CPU baseline)
+#     kt       rocprofv3 --kernel-trace --stats of the default bench command
+#     pmc      FETCH / WRITE / SQ passes for configs D and C (then: python tools/pmc_summary.py gpurun_out TAG{D,C} {D,C} r02)
+#     configs  bench lines of configs A, B, C, E and the batch sweep 1024 / 4096
+#     kernels  hybrid A* and point-formulation throughput
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+T=$1; shift
+( while true; do date >> gpurun_out/heartbeat.log; sleep 20; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+run() {  # name, limit, command...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > gpurun_out/${T}_$name.out 2> gpurun_out/${T}_$name.err
+  local rc=$?; echo "$name rc=$rc"; grep -v amdgpu.ids gpurun_out/${T}_$name.out | tail -3 | cut -c1-300
+  [ $rc -eq 0 ] || exit $rc
+}
+for S in "$@"; do
+  case $S in
+    tests) run gputest 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+           run smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 400 python -u bench.py ;;
+    kt) run kt 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_kt -o kt -- python3 bench.py --no-cpu-baseline ;;
+    pmc) bash tools/gpu_pmc.sh ${T}D --batch 4096 || exit 1
+         bash tools/gpu_pmc.sh ${T}C --config C --batch 4096 || exit 1 ;;
+    configs) run benchA 200 python -u bench.py --config A --steps 2 --no-cpu-baseline
+             run benchB 200 python -u bench.py --config B --steps 2 --no-cpu-baseline
+             run benchC 300 python -u bench.py --config C --steps 2 --no-cpu-baseline
+             run benchE 500 python -u bench.py --config E --steps 1 --warmup 0 --no-cpu-baseline
+             run b1024 200 python -u bench.py --batch 1024 --no-cpu-baseline
+             run b4096 200 python -u bench.py --batch 4096 --no-cpu-baseline ;;
+    kernels) run hastar 300 python -u tools/bench_hastar.py
+             run points 300 python -u tools/bench_points.py ;;
+    *) echo "unknown step $S"; exit 2 ;;
+  esac
+done
