@@ -7,6 +7,7 @@
 #     pmc      FETCH / WRITE / SQ passes for configs D and C (then: python tools/pmc_summary.py gpurun_out TAG{D,C} {D,C} r02)
 #     configs  bench lines of configs A, B, C, E and the batch sweep 1024 / 4096
 #     kernels  hybrid A* and point-formulation throughput
+#     ws2      2-rank rehearsal of the multi-GPU bench on one GPU (gloo: RCCL refuses two ranks on one device)
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
@@ -38,6 +39,8 @@ for S in "$@"; do
              run b4096 200 python -u bench.py --batch 4096 --no-cpu-baseline ;;
     kernels) run hastar 300 python -u tools/bench_hastar.py
              run points 300 python -u tools/bench_points.py ;;
+    ws2) HTP_DIST_BACKEND=gloo run ws2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+           --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --batch 4096 --steps 2 --waves 512 --gen-procs 8 ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done
