@@ -72,7 +72,13 @@ __device__ __forceinline__ bool claim(const WorkSrc& w, long long& t, long long&
     pid = t;
     return t < w.n_static;
   }
-  if (threadIdx.x == 0) __hip_atomic_store(&w.q->claimed, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) {  // claimed = max(claimed, t + 1): a monotone hint (compare-and-swap, a PCIe atomic)
+    long long cur = __hip_atomic_load(&w.q->claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    while (cur < t + 1 &&
+           !__hip_atomic_compare_exchange_strong(&w.q->claimed, &cur, t + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM)) {
+    }
+  }
   const long long t0 = (long long)wall_clock64();
   int ok = 0;
   for (;;) {
@@ -290,8 +296,18 @@ bool uniform44(const Dims& D) {
 }
 
 // Shared launch path of the static-range and queue modes.
+// One launch in flight per context: the ticket counter, the per-wave workspace and the result
+// scratch belong to the context, so a second launch (any stream) before the previous one has
+// completed would share them.  Rejected loudly instead.
+int check_idle(htp_ctx* ctx) {
+  if (ctx->ev1 && hipEventQuery(ctx->ev1) == hipErrorNotReady)
+    return fail(ctx, "[OBCA] a solve launch of this context is still running (one launch in flight per htp_ctx)");
+  return 0;
+}
+
 int launch_solve(htp_ctx* ctx, const htp_obca_batch* in, const htp_obca_result* out, hipStream_t s, WorkSrc src,
                  int64_t waves, bool keep_results) {
+  if (check_idle(ctx)) return -1;
   Dims D;
   make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
   Layout L = make_layout(D);
@@ -506,6 +522,7 @@ int htp_obca_points_solve_batch_device(htp_ctx* ctx, const htp_obca_points_batch
   Dims D;
   make_dims_points(D, in->N, in->M, in->n_vertices, in->obs_edges);
   Layout L = make_layout(D);
+  if (check_idle(ctx)) return -1;
   if (ensure(ctx, &ctx->ws, &ctx->ws_bytes, (size_t)L.total * sizeof(double) * (size_t)in->batch)) return -1;
   if (ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, sizeof(Result) * (size_t)in->batch)) return -1;
   if (!ctx->shape) HIPCHK(hipMalloc((void**)&ctx->shape, sizeof(Shape)));

@@ -4266,7 +4266,6 @@ struct ObcaSolver {
                            e0.comp / sfm <= o.compl_inf_tol;
       const bool acc_lvl = nlp_err <= o.acceptable_tol && e0.dual / sfm <= o.acceptable_dual_inf_tol &&
                            uv <= o.acceptable_constr_viol_tol && e0.comp / sfm <= o.acceptable_compl_inf_tol;
-      if (wall_limit > 0.0 && (double)(c.wall() - t_start) > wall_limit) { status = ST_CPUTIME; break; }
       if (rs) {
         if (!rs_first && resto_converged()) {
           leave_resto();
@@ -4290,6 +4289,9 @@ struct ObcaSolver {
         }
       }
       if (it >= o.max_iter) { status = ST_MAXITER; break; }
+      // max_cpu_time after the convergence / acceptable / iteration-limit tests, in IPOPT's
+      // OptimalityErrorConvergenceCheck order (and after RestoConvergenceCheck in the restoration phase)
+      if (wall_limit > 0.0 && (double)(c.wall() - t_start) > wall_limit) { status = ST_CPUTIME; break; }
       rs_first = false;
       // monotone barrier update (a tiny step forces a decrease)
       bool stop_tiny = false;

@@ -147,6 +147,14 @@ class ObcaNLP:
                     la0 = self.oLAM + i * self.lam_count + n * self.TEo + self.off_o[m]
                     P.append((i, m, n, mu0, la0))
         self.pairs = P
+        # pairs of one (obstacle m, body n) share A, b, G, g: the vectorised loops run per group
+        pi = np.array([q[0] for q in P], dtype=int)
+        self.pgroups = []
+        for m in range(M):
+            for n in range(K):
+                sel = np.arange(len(P))[m * K + n::M * K]
+                self.pgroups.append((m, n, sel, pi[sel], np.array([P[q][3] for q in sel], dtype=int),
+                                     np.array([P[q][4] for q in sel], dtype=int)))
 
     def _build_bounds(self):
         inst, N = self.inst, self.N
@@ -292,14 +300,18 @@ class ObcaNLP:
             F = dynamics(self._stage_w(x), self.dT, self.L, self.topt)
             out[self.gDyn:self.gTerm] = (X[1:] - F).reshape(-1)
         out[self.gTerm:self.gCol] = X[-1] - self.end_state + s
-        for p, (i, m, n, mu0, la0, A, b, G, g, mu, la, st) in enumerate(self._pair_vals(x)):
-            w = A.T @ la
-            c, sn = np.cos(st[3]), np.sin(st[3])
-            r = self.gCol + 4 * p
-            out[r] = w @ w
-            out[r + 1] = G[:, 0] @ mu + (c * w[0] + sn * w[1])
-            out[r + 2] = G[:, 1] @ mu + (-sn * w[0] + c * w[1])
-            out[r + 3] = -g @ mu + (A @ st[:2] - b) @ la
+        for (m, n, sel, i, mu0, la0) in self.pgroups:
+            A, b, G, g = self.A[m], self.b[m], self.G[n], self.gb[n]
+            la = x[la0[:, None] + np.arange(len(b))]
+            mu = x[mu0[:, None] + np.arange(len(g))]
+            st = X[i]
+            w = la @ A
+            c, sn = np.cos(st[:, 3]), np.sin(st[:, 3])
+            r = self.gCol + 4 * sel
+            out[r] = w[:, 0] * w[:, 0] + w[:, 1] * w[:, 1]
+            out[r + 1] = mu @ G[:, 0] + (c * w[:, 0] + sn * w[:, 1])
+            out[r + 2] = mu @ G[:, 1] + (-sn * w[:, 0] + c * w[:, 1])
+            out[r + 3] = -(mu @ g) + np.einsum("pj,pj->p", st[:, :2] @ A.T - b, la)
         return out
 
     def jac(self, x):
@@ -308,9 +320,9 @@ class ObcaNLP:
         rows, cols, vals = [], [], []
 
         def put(r, c, v):
-            rows.append(np.atleast_1d(r))
-            cols.append(np.atleast_1d(c))
-            vals.append(np.atleast_1d(np.asarray(v, dtype=np.float64)))
+            rows.append(np.ravel(r))
+            cols.append(np.ravel(c))
+            vals.append(np.ravel(np.asarray(v, dtype=np.float64)))
 
         put(np.arange(NS), np.arange(NS), np.ones(NS))
         if N > 1:
@@ -328,25 +340,28 @@ class ObcaNLP:
                 put(rr, cc, -Jd[i].reshape(-1))
         put(self.gTerm + np.arange(NS), NS * (N - 1) + np.arange(NS), np.ones(NS))
         put(self.gTerm + np.arange(NS), self.oS + np.arange(NS), np.ones(NS))
-        for p, (i, m, n, mu0, la0, A, b, G, g, mu, la, st) in enumerate(self._pair_vals(x)):
-            w = A.T @ la
-            c, sn = np.cos(st[3]), np.sin(st[3])
-            r = self.gCol + 4 * p
+        X = x[: NS * N].reshape(N, NS)
+        for (m, n, sel, i, mu0, la0) in self.pgroups:
+            A, b, G, g = self.A[m], self.b[m], self.G[n], self.gb[n]
             em, en = len(b), len(g)
-            lai = la0 + np.arange(em)
-            mui = mu0 + np.arange(en)
-            put(np.full(em, r), lai, 2.0 * A @ w)
-            # c2 = G^T mu + R^T A^T lam
-            put(np.full(en, r + 1), mui, G[:, 0])
-            put(np.full(en, r + 2), mui, G[:, 1])
-            put(np.full(em, r + 1), lai, c * A[:, 0] + sn * A[:, 1])
-            put(np.full(em, r + 2), lai, -sn * A[:, 0] + c * A[:, 1])
-            put(r + 1, NS * i + 3, -sn * w[0] + c * w[1])
-            put(r + 2, NS * i + 3, -c * w[0] - sn * w[1])
-            # c3 = -g.mu + (A t - b).lam
-            put(np.full(en, r + 3), mui, -g)
-            put(np.full(em, r + 3), lai, A @ st[:2] - b)
-            put([r + 3, r + 3], [NS * i, NS * i + 1], w)
+            la = x[la0[:, None] + np.arange(em)]
+            st = X[i]
+            w = la @ A
+            c, sn = np.cos(st[:, 3]), np.sin(st[:, 3])
+            r = (self.gCol + 4 * sel)[:, None]
+            lai = la0[:, None] + np.arange(em)
+            mui = mu0[:, None] + np.arange(en)
+            one_e, one_n = np.ones((1, em)), np.ones((1, en))
+            put((r * one_e).ravel(), lai.ravel(), (2.0 * w @ A.T).ravel())
+            put((r + 1) * one_n, mui, np.broadcast_to(G[:, 0], mui.shape))
+            put((r + 2) * one_n, mui, np.broadcast_to(G[:, 1], mui.shape))
+            put((r + 1) * one_e, lai, c[:, None] * A[:, 0] + sn[:, None] * A[:, 1])
+            put((r + 2) * one_e, lai, -sn[:, None] * A[:, 0] + c[:, None] * A[:, 1])
+            put(r[:, 0] + 1, NS * i + 3, -sn * w[:, 0] + c * w[:, 1])
+            put(r[:, 0] + 2, NS * i + 3, -c * w[:, 0] - sn * w[:, 1])
+            put((r + 3) * one_n, mui, np.broadcast_to(-g, mui.shape))
+            put((r + 3) * one_e, lai, st[:, :2] @ A.T - b)
+            put(np.repeat(r[:, 0] + 3, 2), (NS * i[:, None] + np.arange(2)).ravel(), w.ravel())
         Jm = sp.coo_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
                            shape=(self.m, self.n))
         return Jm.tocsr()
@@ -412,28 +427,28 @@ class ObcaNLP:
                 ci = np.array(cidx)
                 add(ci[:, None], ci[None, :], Hd[i])
 
-        for p, (i, m, n, mu0, la0, A, b, G, g, mu, la, st) in enumerate(self._pair_vals(x)):
-            r = self.gCol + 4 * p
-            y1, y2a, y2b, y3 = y[r], y[r + 1], y[r + 2], y[r + 3]
-            w = A.T @ la
-            c, sn = np.cos(st[3]), np.sin(st[3])
+        for (m, n, sel, i, mu0, la0) in self.pgroups:
+            A, b = self.A[m], self.b[m]
             em = len(b)
-            lai = la0 + np.arange(em)
+            r = self.gCol + 4 * sel
+            y1, y2a, y2b, y3 = y[r], y[r + 1], y[r + 2], y[r + 3]
+            la = x[la0[:, None] + np.arange(em)]
+            w = la @ A
+            c, sn = np.cos(X[i, 3]), np.sin(X[i, 3])
+            lai = la0[:, None] + np.arange(em)
             th = NS * i + 3
-            add(lai[:, None], lai[None, :], y1 * 2.0 * A @ A.T)
-            # d/dlam of y2^T dR^T/dth A^T lam
-            dRt = np.array([[-sn, c], [-c, -sn]])
-            yv = np.array([y2a, y2b])
-            v_thl = A @ (dRt.T @ yv)
-            add(lai, th, v_thl)
-            add(th, lai, v_thl)
+            AA = 2.0 * A @ A.T
+            add(lai[:, :, None], lai[:, None, :], y1[:, None, None] * AA)
+            # d/dlam of y2^T dR^T/dth A^T lam:  dR^T' y2 = [-sn y2a - c y2b, c y2a - sn y2b]
+            gx, gy = -sn * y2a - c * y2b, c * y2a - sn * y2b
+            v_thl = gx[:, None] * A[:, 0] + gy[:, None] * A[:, 1]
+            add(lai, th[:, None], v_thl)
+            add(th[:, None], lai, v_thl)
             # d2/dth2: -y2^T R^T w
-            Rt = np.array([[c, sn], [-sn, c]])
-            add(th, th, -(yv @ (Rt @ w)))
-            # (x, y)-lam from c3
+            add(th, th, -(y2a * (c * w[:, 0] + sn * w[:, 1]) + y2b * (-sn * w[:, 0] + c * w[:, 1])))
             for k in range(2):
-                add(lai, NS * i + k, y3 * A[:, k])
-                add(NS * i + k, lai, y3 * A[:, k])
+                add(lai, (NS * i + k)[:, None], y3[:, None] * A[:, k])
+                add((NS * i + k)[:, None], lai, y3[:, None] * A[:, k])
         Hm = sp.coo_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
                            shape=(self.n, self.n))
         return Hm.tocsr()

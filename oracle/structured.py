@@ -47,7 +47,9 @@ def _eig_inertia(Ms):
     return int(pos), int(neg), int(zer)
 
 
-class StructuredKKT:
+class StructuredKKTLoop:
+    """Per-block reference loop (the round-1/2 oracle); kept to cross-check StructuredKKT."""
+
     def __init__(self, nlp):
         self.nlp = nlp
         N = nlp.N
@@ -200,6 +202,213 @@ class StructuredKKT:
             w = Kib - KiB @ dx[p]
             dx[z] = w[:z.size]
             dyc[rows] = w[z.size:]
+        dyd = (Jd @ dx - bd - bs / Ds) / Ed
+        ds = (bs + dyd) / Ds
+        return dx, ds, dyc, dyd
+
+
+def _gather(M, R, C):
+    """Dense values M[R, C] of a CSR matrix for broadcast index arrays R, C."""
+    R, C = np.broadcast_arrays(np.asarray(R), np.asarray(C))
+    if R.size == 0:
+        return np.zeros(R.shape)
+    return np.asarray(M[R.ravel(), C.ravel()]).reshape(R.shape)
+
+
+def _ldl_nopiv(K):
+    """Batched unpivoted LDL^T pivots of symmetric K (B, n, n) -> d (B, n) (no interchanges)."""
+    A = K.copy()
+    n = A.shape[1]
+    d = np.zeros(A.shape[:2])
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        for k in range(n):
+            d[:, k] = A[:, k, k]
+            if k + 1 < n:
+                l = A[:, k + 1:, k] / d[:, k, None]
+                A[:, k + 1:, k + 1:] -= l[:, :, None] * A[:, None, k, k + 1:]
+    return d
+
+
+class StructuredKKT:
+    """Same elimination and inertia as StructuredKKTLoop, batched over the collision pairs.
+
+    The pairs of one (obstacle m, body n) share a block shape and are handled as one stack:
+    the dense blocks are gathered from the sparse matrices in one indexing call, the inertia of
+    a block comes from its unpivoted LDL^T when every multiplier pivot is positive (then the
+    block is [H, C'; C, -dc] with H positive definite, a stable factorisation whose pivot signs
+    are the exact inertia) and from the Bunch-Kaufman LDL^T otherwise, and the solves run
+    through numpy's batched LU.  Schur complements enter the stage blocks in the loop
+    version's order (pairs of stage i in (m, n) order, then the terminal block)."""
+
+    def __init__(self, nlp):
+        self.nlp = nlp
+        N = nlp.N
+        gL, gU = nlp.g_L, nlp.g_U
+        E = np.where(gL == gU)[0]
+        posE = -np.ones(nlp.m, dtype=int)
+        posE[E] = np.arange(E.size)
+        self.posE = posE
+        P = len(nlp.pairs)
+        pi = np.array([q[0] for q in nlp.pairs], dtype=int)
+        pm = np.array([q[1] for q in nlp.pairs], dtype=int)
+        pn = np.array([q[2] for q in nlp.pairs], dtype=int)
+        mu0 = np.array([q[3] for q in nlp.pairs], dtype=int)
+        la0 = np.array([q[4] for q in nlp.pairs], dtype=int)
+        self.groups = []
+        for m in range(nlp.M):
+            for n in range(nlp.K):
+                sel = np.where((pm == m) & (pn == n))[0]
+                if sel.size == 0:
+                    continue
+                en, em = int(nlp.eb[n]), int(nlp.eo[m])
+                Z = np.concatenate([mu0[sel, None] + np.arange(en), la0[sel, None] + np.arange(em)], axis=1)
+                r = nlp.gCol + 4 * sel
+                Rw = posE[np.stack([r + 1, r + 2], axis=1)]
+                Pv = np.stack([NS * pi[sel], NS * pi[sel] + 1, NS * pi[sel] + 3], axis=1)
+                self.groups.append(dict(sel=sel, stage=pi[sel], Z=Z, R=Rw, P=Pv))
+        self.npair = P
+        self.term = (nlp.oS + np.arange(NS), posE[nlp.gTerm + np.arange(NS)], NS * (N - 1) + np.arange(NS))
+        self.stage_vars, self.stage_rows = [], []
+        for i in range(N):
+            v = list(NS * i + np.arange(NS))
+            if i < N - 1:
+                v += [nlp.oU + NC * i, nlp.oU + NC * i + 1]
+                if nlp.topt:
+                    v.append(nlp.oTAU + i)
+            rows = np.arange(NS) if i == 0 else nlp.gDyn + NS * (i - 1) + np.arange(NS)
+            self.stage_vars.append(np.array(v))
+            self.stage_rows.append(posE[rows])
+        self.n_stage = sum(len(v) for v in self.stage_vars)
+
+    def factor(self, Wm, Sx, Ss, Jc, Jd, dw, dc):
+        import scipy.sparse as sp
+        nlp = self.nlp
+        Wm, Jc, Jd = Wm.tocsr(), Jc.tocsr(), Jd.tocsr()
+        n, mc, md = Wm.shape[0], Jc.shape[0], Jd.shape[0]
+        dcv = np.broadcast_to(np.asarray(dc, dtype=float), (mc + md,))
+        dcc, dcd = dcv[:mc], dcv[mc:]
+        Ds = Ss + dw
+        Ed = 1.0 / Ds + dcd
+        Hb = (Wm + sp.diags(Sx + dw) + Jd.T @ sp.diags(1.0 / Ed) @ Jd).tocsr()
+        self._Hb, self._Jc, self._Jd, self._Ds, self._Ed, self._dc = Hb, Jc, Jd, Ds, Ed, dc
+        pos, neg, zer = md, md, 0
+        N = nlp.N
+        schur = np.zeros((N, 3, 3))
+        self.gfac = []
+        for g in self.groups:
+            Z, Rw, Pv = g["Z"], g["R"], g["P"]
+            nz, nr = Z.shape[1], Rw.shape[1]
+            B_ = Z.shape[0]
+            K = np.zeros((B_, nz + nr, nz + nr))
+            K[:, :nz, :nz] = _gather(Hb, Z[:, :, None], Z[:, None, :])
+            Cz = _gather(Jc, Rw[:, :, None], Z[:, None, :])
+            K[:, nz:, :nz] = Cz
+            K[:, :nz, nz:] = np.transpose(Cz, (0, 2, 1))
+            K[:, nz:, nz:] = -dcc[Rw][:, :, None] * np.eye(nr)
+            Bm = np.concatenate([_gather(Hb, Z[:, :, None], Pv[:, None, :]),
+                                 _gather(Jc, Rw[:, :, None], Pv[:, None, :])], axis=1)
+            d = _ldl_nopiv(K)
+            ok = np.all(d[:, :nz] > 0, axis=1) & np.all(np.isfinite(d), axis=1) & np.all(d != 0, axis=1)
+            pos += int(np.sum(d[ok] > 0))
+            neg += int(np.sum(d[ok] < 0))
+            for b in np.where(~ok)[0]:
+                a, b_, c_ = _eig_inertia(K[b])
+                pos, neg, zer = pos + a, neg + b_, zer + c_
+            if zer:
+                return pos, neg, zer
+            KiB = np.linalg.solve(K, Bm)
+            S = np.einsum("bki,bkj->bij", Bm, KiB)
+            np.add.at(schur, g["stage"], S)
+            self.gfac.append((K, Bm, KiB))
+        # terminal block
+        z, rows, p = self.term
+        nz, nr = z.size, rows.size
+        K = np.zeros((nz + nr, nz + nr))
+        K[:nz, :nz] = _gather(Hb, z[:, None], z[None, :])
+        Cz = _gather(Jc, rows[:, None], z[None, :])
+        K[nz:, :nz] = Cz
+        K[:nz, nz:] = Cz.T
+        K[nz:, nz:] = -np.diag(dcc[rows])
+        Bt = np.vstack([_gather(Hb, z[:, None], p[None, :]), _gather(Jc, rows[:, None], p[None, :])])
+        a, b_, c_ = _eig_inertia(K)
+        pos, neg, zer = pos + a, neg + b_, zer + c_
+        if c_:
+            return pos, neg, zer
+        KiBt = np.linalg.solve(K, Bt)
+        self.tfac = (K, Bt, KiBt)
+        St = Bt.T @ KiBt
+        # stage blocks
+        self.D, self.Lo = [], []
+        prev = None
+        sidx = np.array([0, 1, 3])
+        for i in range(N):
+            v, r = self.stage_vars[i], self.stage_rows[i]
+            nv, nr = v.size, r.size
+            K = np.zeros((nr + nv, nr + nv))
+            K[:nr, :nr] = -np.diag(dcc[r])
+            Jr = _gather(Jc, r[:, None], v[None, :])
+            K[:nr, nr:] = Jr
+            K[nr:, :nr] = Jr.T
+            K[nr:, nr:] = _gather(Hb, v[:, None], v[None, :])
+            if self.npair:
+                K[np.ix_(nr + sidx, nr + sidx)] -= schur[i]
+            if i == N - 1:
+                K[nr:nr + NS, nr:nr + NS] -= St
+            if prev is not None:
+                pv, pr, Dp = prev
+                Off = np.zeros((nr + nv, pr.size + pv.size))
+                Off[:nr, pr.size:] = _gather(Jc, r[:, None], pv[None, :])
+                Off[nr:, pr.size:] = _gather(Hb, v[:, None], pv[None, :])
+                LD = np.linalg.solve(Dp, Off.T).T
+                K = K - LD @ Off.T
+                self.Lo.append((Off, LD))
+            a, b_, c_ = _eig_inertia(K)
+            pos, neg, zer = pos + a, neg + b_, zer + c_
+            self.D.append(K)
+            prev = (v, r, K)
+        return pos, neg, zer
+
+    def solve(self, bx, bs, bc, bd):
+        nlp = self.nlp
+        Jd, Ds, Ed = self._Jd, self._Ds, self._Ed
+        bxb = bx + Jd.T @ ((bd + bs / Ds) / Ed)
+        bcb = bc.copy()
+        srhs = np.zeros(nlp.n)
+        kibs = []
+        for g, (K, Bm, KiB) in zip(self.groups, self.gfac):
+            bl = np.concatenate([bxb[g["Z"]], bcb[g["R"]]], axis=1)
+            Kib = np.linalg.solve(K, bl[:, :, None])[:, :, 0]
+            kibs.append(Kib)
+            np.add.at(srhs, g["P"], np.einsum("bkj,bk->bj", Bm, Kib))
+        z, rows, p = self.term
+        Kt, Bt, KiBt = self.tfac
+        Kibt = np.linalg.solve(Kt, np.concatenate([bxb[z], bcb[rows]]))
+        srhs[p] += Bt.T @ Kibt
+        N = nlp.N
+        V = []
+        for i in range(N):
+            v, r = self.stage_vars[i], self.stage_rows[i]
+            rv = np.concatenate([bcb[r], bxb[v] - srhs[v]])
+            V.append(rv if i == 0 else rv - self.Lo[i - 1][1] @ V[i - 1])
+        X = [None] * N
+        X[N - 1] = np.linalg.solve(self.D[N - 1], V[N - 1])
+        for i in range(N - 2, -1, -1):
+            Off, LD = self.Lo[i]
+            X[i] = np.linalg.solve(self.D[i], V[i] - Off.T @ X[i + 1])
+        dx = np.zeros(nlp.n)
+        dyc = np.zeros(bc.size)
+        for i in range(N):
+            v, r = self.stage_vars[i], self.stage_rows[i]
+            dyc[r] = X[i][:r.size]
+            dx[v] = X[i][r.size:]
+        for g, (K, Bm, KiB), Kib in zip(self.groups, self.gfac, kibs):
+            w = Kib - np.einsum("bij,bj->bi", KiB, dx[g["P"]])
+            nz = g["Z"].shape[1]
+            dx[g["Z"]] = w[:, :nz]
+            dyc[g["R"]] = w[:, nz:]
+        w = Kibt - KiBt @ dx[p]
+        dx[z] = w[:z.size]
+        dyc[rows] = w[z.size:]
         dyd = (Jd @ dx - bd - bs / Ds) / Ed
         ds = (bs + dyd) / Ds
         return dx, ds, dyc, dyd

@@ -17,6 +17,7 @@ import os
 import numpy as np
 import pytest
 
+from _fixture_io import has_instance, load_instance
 from headland_trajectory_planning_amd import _native, synth
 from oracle.ipm import IpoptRestatement
 from oracle.nlp import ObcaNLP
@@ -67,18 +68,21 @@ def _golden():
 
 @pytest.mark.parametrize("cfg,pid,path", _golden(), ids=lambda v: str(v) if not str(v).endswith(".npz") else "")
 def test_full_config_parity_vs_oracle_fixtures(ctx, cfg, pid, path):
+    """Fixtures hold their own input (tests/_fixture_io.py).  Converged problems: status, states
+    <= 1e-4, objective <= 1e-6 rel.  Problems the oracle does NOT solve (infeasible / restoration
+    failed / iteration limit, max_cpu_time off): the GPU must end with the same status."""
     g = np.load(path)
     _, N, M, imp = synth.CONFIGS[cfg]
     assert int(g["N"]) == N
-    inst = synth.config_instance(cfg, pid)
-    if "turn" in g.files:
-        assert inst["meta"]["turn"] == str(g["turn"])
+    inst = load_instance(g) if has_instance(g) else synth.config_instance(cfg, pid)
     res = ctx.solve(_native.PackedBatch([inst]))
-    assert res.status[0] == int(g["status"]) and res.status[0] in (0, 1), (res.status[0], int(g["status"]))
-    assert np.max(np.abs(res.x[0, :5 * N] - g["states"])) <= STATE_TOL
-    assert abs(res.objective[0] - float(g["f"])) <= 1e-6 * max(1.0, abs(float(g["f"])))
+    st = int(g["status"])
+    assert res.status[0] == st, (res.status[0], st, int(res.iterations[0]), int(g["iters"]))
     # the restoration phases the oracle needed are taken on the device too
     assert (res.n_resto[0] > 0) == (int(g["n_resto"]) > 0)
+    if st in (0, 1):
+        assert np.max(np.abs(res.x[0, :5 * N] - g["states"])) <= STATE_TOL
+        assert abs(res.objective[0] - float(g["f"])) <= 1e-6 * max(1.0, abs(float(g["f"])))
 
 
 def _kkt_residuals(nlp, x):

@@ -28,7 +28,8 @@ for S in "$@"; do
     tests) run gputest 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
            run smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python -u bench.py ;;
-    kt) run kt 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_kt -o kt -- python3 bench.py --no-cpu-baseline ;;
+    kt) run ktgen 300 python -u bench.py --gen-only --cache /tmp/htp_instcache
+        run kt 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_kt -o kt -- python3 bench.py --no-cpu-baseline --cache /tmp/htp_instcache ;;
     pmc) bash tools/gpu_pmc.sh ${T}D --batch 4096 || exit 1
          bash tools/gpu_pmc.sh ${T}C --config C --batch 4096 || exit 1 ;;
     configs) run benchA 200 python -u bench.py --config A --steps 2 --no-cpu-baseline

@@ -11,8 +11,13 @@ ARGS=${*:---batch 4096}
 ( while true; do date >> gpurun_out/heartbeat.log; sleep 20; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
+# instances: generated once with the normal parallel (fork-pool) generator, OUTSIDE the profiler
+# (rocprofv3's preloaded library brings the GPU up before bench.py starts, so the profiled
+# process must not fork); the profiled runs load them from the cache
+CACHE=/tmp/htp_instcache
+timeout -k 10 300 python3 bench.py --gen-only --cache $CACHE $ARGS > gpurun_out/${TAG}_gen.log 2>&1 || exit 1
 pass() {  # name, counters
-  timeout -s KILL 300 rocprofv3 --pmc $2 --output-format csv -d gpurun_out/${TAG}_pmc_$1 -o $1 -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --gen-procs 1 $ARGS > gpurun_out/${TAG}_pmc_$1.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc $2 --output-format csv -d gpurun_out/${TAG}_pmc_$1 -o $1 -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --cache $CACHE $ARGS > gpurun_out/${TAG}_pmc_$1.log 2>&1
   rc=$?; echo "$1 rc=$rc"; return $rc
 }
 pass fetch FETCH_SIZE || exit 1
