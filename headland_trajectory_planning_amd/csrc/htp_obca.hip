@@ -103,7 +103,9 @@ __device__ __forceinline__ bool claim(const WorkSrc& w, long long& t, long long&
 // One wavefront per problem at a time; each wave keeps claiming tickets until
 // its work source is exhausted, so a long solve holds one wave and never the
 // launch (no per-launch tail); the workspace is per wave, not per problem.
-template <int EN, int EM>
+// FORM 0: optimizer.py (EN, EM edges of the body / obstacle polytopes); FORM 1: the point
+// formulation of optimizer_points.py (lambda-only local blocks, EN unused).
+template <int EN, int EM, int FORM>
 __global__ __launch_bounds__(64, HTP_WAVES_PER_EU) void obca_solve_kernel(const Shape* __restrict__ shp, BatchView b,
                                                         double* __restrict__ ws_all, int64_t ws_stride,
                                                         Result* __restrict__ res, double* __restrict__ xout,
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(64, HTP_WAVES_PER_EU) void obca_solve_kernel(const 
   while (claim(src, t, p)) {
     DevWave c{(int)threadIdx.x, lds, ilds};
     ProblemIn in = problem_view(b, sh->D, p);
-    ObcaSolver<DevWave, EN, EM> S(c, sh->D, sh->L, sh->o, in, ws);
+    ObcaSolver<DevWave, EN, EM, FORM> S(c, sh->D, sh->L, sh->o, in, ws);
     Result r{};
     S.run(r);
     if (threadIdx.x == 0) {
@@ -136,44 +138,6 @@ __global__ __launch_bounds__(64, HTP_WAVES_PER_EU) void obca_solve_kernel(const 
     for (int q = threadIdx.x; q < n; q += 64) xout[p * n + q] = x[q];
     c.sync();
   }
-}
-
-// point formulation (optimizer_points.py): the same IPM, lambda-only local blocks
-template <int EM>
-__global__ __launch_bounds__(64, HTP_WAVES_PER_EU) void obca_points_kernel(const Shape* __restrict__ shp, BatchView b,
-                                                                          double* __restrict__ ws_all,
-                                                                          int64_t ws_stride, Result* __restrict__ res,
-                                                                          double* __restrict__ xout, int batch) {
-  __shared__ double lds_[LDS_D];
-  __shared__ int ilds_[2 * NBMAX];
-  DevWave::ld* lds = (DevWave::ld*)lds_;
-  DevWave::li* ilds = (DevWave::li*)ilds_;
-  const int p = blockIdx.x;
-  if (p >= batch) return;
-  DevWave c{(int)threadIdx.x, lds, ilds};
-  using CS = DevWave::cst<Shape>;
-  CS* sh = (CS*)shp;
-  ProblemIn in = problem_view(b, sh->D, p);
-  double* ws = ws_all + (int64_t)p * ws_stride;
-  ObcaSolver<DevWave, 1, EM, 1> S(c, sh->D, sh->L, sh->o, in, ws);
-  Result r{};
-  S.run(r);
-  if (threadIdx.x == 0) res[p] = r;
-  const double* x = ws + sh->L.x;
-  const int n = sh->D.n;
-  for (int q = threadIdx.x; q < n; q += 64) xout[(int64_t)p * n + q] = x[q];
-}
-
-__global__ void unpack_results(const Result* __restrict__ r, int batch, double* obj, int32_t* st, int32_t* it,
-                               int32_t* nf, double* err, int32_t* nrs) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= batch) return;
-  if (obj) obj[p] = r[p].objective;
-  if (st) st[p] = r[p].status;
-  if (it) it[p] = r[p].iters;
-  if (nf) nf[p] = r[p].n_factor;
-  if (err) err[p] = r[p].nlp_error;
-  if (nrs) nrs[p] = r[p].n_resto;
 }
 
 }  // namespace
@@ -280,10 +244,10 @@ struct htp_queue {
 
 namespace {
 
-template <int EN, int EM>
+template <int EN, int EM, int FORM = 0>
 int resident_waves_t(htp_ctx* ctx, unsigned pad) {
   int per_cu = 0, cus = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)obca_solve_kernel<EN, EM>, 64, pad));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)obca_solve_kernel<EN, EM, FORM>, 64, pad));
   HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
   return per_cu * cus > 0 ? per_cu * cus : 1;
 }
@@ -331,14 +295,14 @@ int launch_solve(htp_ctx* ctx, const htp_obca_batch* in, const htp_obca_result* 
   HIPCHK(hipEventRecord(ctx->ev0, s));
   Result* res = keep_results ? (Result*)ctx->scratch : nullptr;
   if (u44) {
-    if (pad) HIPCHK(hipFuncSetAttribute((const void*)obca_solve_kernel<4, 4>,
+    if (pad) HIPCHK(hipFuncSetAttribute((const void*)obca_solve_kernel<4, 4, 0>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad));
-    hipLaunchKernelGGL((obca_solve_kernel<4, 4>), dim3((unsigned)waves), dim3(64), pad, s, (const Shape*)ctx->shape, b,
+    hipLaunchKernelGGL((obca_solve_kernel<4, 4, 0>), dim3((unsigned)waves), dim3(64), pad, s, (const Shape*)ctx->shape, b,
                        (double*)ctx->ws, (int64_t)L.total, res, out->x, src, ov);
   } else {
-    if (pad) HIPCHK(hipFuncSetAttribute((const void*)obca_solve_kernel<MAXE, MAXE>,
+    if (pad) HIPCHK(hipFuncSetAttribute((const void*)obca_solve_kernel<MAXE, MAXE, 0>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad));
-    hipLaunchKernelGGL((obca_solve_kernel<MAXE, MAXE>), dim3((unsigned)waves), dim3(64), pad, s,
+    hipLaunchKernelGGL((obca_solve_kernel<MAXE, MAXE, 0>), dim3((unsigned)waves), dim3(64), pad, s,
                        (const Shape*)ctx->shape, b, (double*)ctx->ws, (int64_t)L.total, res, out->x, src, ov);
   }
   HIPCHK(hipGetLastError());
@@ -518,34 +482,41 @@ int htp_obca_points_solve_batch_device(htp_ctx* ctx, const htp_obca_points_batch
   const char* e = nullptr;
   if (check_shape_points(in, &e)) return fail(ctx, e);
   if (in->batch == 0) return 0;
+  if (!out->x) return fail(ctx, "[OBCA] out->x is required");
   HIPCHK(hipSetDevice(ctx->device));
+  if (check_idle(ctx)) return -1;
   Dims D;
   make_dims_points(D, in->N, in->M, in->n_vertices, in->obs_edges);
   Layout L = make_layout(D);
-  if (check_idle(ctx)) return -1;
-  if (ensure(ctx, &ctx->ws, &ctx->ws_bytes, (size_t)L.total * sizeof(double) * (size_t)in->batch)) return -1;
+  bool u4 = true;
+  for (int m = 0; m < D.M; ++m) u4 = u4 && D.eo[m] == 4;
+  // persistent launch: as many wavefronts as are resident, each claiming problems from the
+  // static ticket range (as obca_solve_kernel for optimizer.py), workspace per wavefront
+  int cap = u4 ? resident_waves_t<1, 4, 1>(ctx, 0) : resident_waves_t<1, MAXE, 1>(ctx, 0);
+  if (cap < 0) return -1;
+  const int64_t waves = cap < in->batch ? cap : in->batch;
+  if (ensure(ctx, &ctx->ws, &ctx->ws_bytes, (size_t)L.total * sizeof(double) * (size_t)waves)) return -1;
   if (ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, sizeof(Result) * (size_t)in->batch)) return -1;
   if (!ctx->shape) HIPCHK(hipMalloc((void**)&ctx->shape, sizeof(Shape)));
+  if (!ctx->next) HIPCHK(hipMalloc((void**)&ctx->next, 256));
   Shape hs{D, L, ctx->opt};
   hs.o.wall_rate = ctx->wall_rate;
   const BatchView b = points_view(in);
   hipStream_t s = (hipStream_t)stream;
+  WorkSrc src{(unsigned long long*)ctx->next, nullptr, (long long)in->batch, 0};
+  OutView ov{out->objective, out->status, out->iterations, out->n_factor, out->nlp_error, out->n_resto};
   HIPCHK(hipMemcpyAsync(ctx->shape, &hs, sizeof(Shape), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(src.next, 0, sizeof(unsigned long long), s));
   HIPCHK(hipEventRecord(ctx->ev0, s));
-  bool u4 = true;
-  for (int m = 0; m < D.M; ++m) u4 = u4 && D.eo[m] == 4;
   if (u4)
-    hipLaunchKernelGGL((obca_points_kernel<4>), dim3(in->batch), dim3(64), 0, s, (const Shape*)ctx->shape, b,
-                       (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
+    hipLaunchKernelGGL((obca_solve_kernel<1, 4, 1>), dim3((unsigned)waves), dim3(64), 0, s, (const Shape*)ctx->shape, b,
+                       (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x, src, ov);
   else
-    hipLaunchKernelGGL((obca_points_kernel<MAXE>), dim3(in->batch), dim3(64), 0, s, (const Shape*)ctx->shape, b,
-                       (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x, in->batch);
+    hipLaunchKernelGGL((obca_solve_kernel<1, MAXE, 1>), dim3((unsigned)waves), dim3(64), 0, s,
+                       (const Shape*)ctx->shape, b, (double*)ctx->ws, (int64_t)L.total, (Result*)ctx->scratch, out->x,
+                       src, ov);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1, s));
-  hipLaunchKernelGGL(unpack_results, dim3((in->batch + 255) / 256), dim3(256), 0, s, (const Result*)ctx->scratch,
-                     in->batch, out->objective, out->status, out->iterations, out->n_factor, out->nlp_error,
-                     out->n_resto);
-  HIPCHK(hipGetLastError());
   return 0;
 }
 

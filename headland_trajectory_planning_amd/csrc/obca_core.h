@@ -295,7 +295,8 @@ HTP_HD inline void bk_solve_packed(T* K, const int* ip, int n, double* v) {
 constexpr int RING_SB = 8;                       // stages per block
 constexpr int RS_SLOT = 142;                     // LD slot prefix (P | K | chol | J | 1/sc)
 constexpr int RS_V = RS_SLOT, RS_X = RS_SLOT + NBMAX;
-constexpr int RS_L = RS_SLOT + 2 * NBMAX;        // doubles per stage record
+constexpr int RS_T = RS_SLOT + 2 * NBMAX;        // T_i, Q_i of the relaxed dynamics rows (relax_P), 5 x 5 each
+constexpr int RS_L = RS_T + 50;                  // doubles per stage record
 constexpr int RING_OFF = 4 * NBMAX * NBMAX + 8 + 2 * 64;
 constexpr int RING_DOUBLES = (RING_SB + 1) * RS_L;
 // pivoted local blocks (ObcaSolver::local_pivoted) on the device: one packed 10x10 block per lane in LDS,
@@ -2144,10 +2145,129 @@ struct ObcaSolver {
     }
   }
 
-  // returns number of stages whose Rt is not positive definite
-  HTP_HD HTP_FI int riccati_factor() {
-    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
+  // ---------------------------------------------- relaxed dynamics rows (restoration, delta_c > 0)
+  // With delta_c > 0 or in the restoration phase (eliminated n/p: e_R on the diagonal) the y rows of
+  // stage block i read  s (x_i - xh_i) - E y_i = b  (xh_i = F_{i-1} u_{i-1} + e_i the nominal state),
+  // i.e.  x_i = xh_i + Eh yh_i  with  Eh = E / s^2  and  yh = s y.  Eliminating y_i (pivot -E: its 5
+  // negative eigenvalues) and then x_i (pivot P_xx + Eh^-1, which must be positive definite for
+  // IPOPT's inertia) turns the cost-to-go (P, p) over z_i into one over the NOMINAL zh_i.  With
+  // S = Eh^1/2, A = S P_xx S, Mi = (I + A)^-1 (Cholesky L L' = I + A):
+  //   P~[x,:] = S^-1 Mi S P[x,:],   P~[c,c] = P[c,c] - W_c' W_c  (W = L^-1 S P[x,:]),
+  //   T = S Mi S = (P_xx + Eh^-1)^-1,   Q = S^-1 Mi S = (I + P_xx Eh)^-1;
+  // no term is a difference of nearly equal numbers whether Eh is tiny (delta_c) or huge (restoration
+  // rows whose n/p are far from their bounds: P~_xx -> Eh^-1, T -> P_xx^-1).  The solve passes use
+  //   backward  w_x = Q r_x,  w_c = r_c - P[c,x] T r_x       (r = p - P e, the exact-dynamics w),
+  //   forward   x_i = xh_i + T r_x,  yh_i = Q r_x             (r = p - P zh).
+  // Exact inertia (Sylvester): every (I + A) and every Rt positive definite.  E = 0 (the
+  // exact-dynamics iterations) is the plain recursion.
+  HTP_HD HTP_FI void stage_Eh(int i, double dc, double* Eh) const {
     const gd* scE = A(L.scE);
+    const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
+    for (int k = 0; k < NS; ++k) {
+      const double e = dc + (rs ? A(L.eR)[rowbase + k] : 0.0);
+      const double sc = scE[rowbase + k];
+      Eh[k] = dmax(e / (sc * sc), 1e-300);
+    }
+  }
+  // Cholesky of a symmetric 5x5 (row-major) into packed lower Lc (15) with RECIPROCAL pivots
+  HTP_HD HTP_FI static bool chol5(const double* Am, double* Lc) {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      double d = Am[j * NS + j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) d -= Lc[j * (j + 1) / 2 + k] * Lc[j * (j + 1) / 2 + k];
+      if (!(d > 0.0)) { ok = false; d = 1.0; }
+      const double id = 1.0 / sqrt(d);
+      Lc[j * (j + 1) / 2 + j] = id;
+#pragma unroll
+      for (int r = j + 1; r < NS; ++r) {
+        double v = Am[r * NS + j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) v -= Lc[r * (r + 1) / 2 + k] * Lc[j * (j + 1) / 2 + k];
+        Lc[r * (r + 1) / 2 + j] = v * id;
+      }
+    }
+    return ok;
+  }
+  HTP_HD HTP_FI static void chol5_fwd(const double* Lc, double* b) {  // b <- L^-1 b
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+#pragma unroll
+      for (int k = 0; k < j; ++k) b[j] -= Lc[j * (j + 1) / 2 + k] * b[k];
+      b[j] *= Lc[j * (j + 1) / 2 + j];
+    }
+  }
+  HTP_HD HTP_FI static void chol5_bwd(const double* Lc, double* b) {  // b <- L^-T b
+#pragma unroll
+    for (int j = NS - 1; j >= 0; --j) {
+#pragma unroll
+      for (int k = j + 1; k < NS; ++k) b[j] -= Lc[k * (k + 1) / 2 + j] * b[k];
+      b[j] *= Lc[j * (j + 1) / 2 + j];
+    }
+  }
+  // P8 (LDS, 8 x 8 stride 8, symmetric): cost-to-go of stage block i -> its relaxed form P~ (in place,
+  // symmetric); T_i to Trec[0, 25) and Q_i to Trec[25, 50) (global) for the solve passes.
+  // Wl: LDS scratch (105 doubles).  Returns false if I + S P_xx S is not positive definite.
+  HTP_HD HTP_FI bool relax_P(ld* P8, int i, double dc, ld* Wl, gd* Trec) {
+    double Eh[NS], S[NS], Am[NS * NS], Lc[15];
+    stage_Eh(i, dc, Eh);
+    for (int k = 0; k < NS; ++k) S[k] = sqrt(Eh[k]);
+    for (int a = 0; a < NS; ++a)
+      for (int b = 0; b < NS; ++b) Am[a * NS + b] = (a == b ? 1.0 : 0.0) + S[a] * P8[a * 8 + b] * S[b];
+    const bool ok = chol5(Am, Lc);
+    ld* Wm = Wl;         // 5 x 8: W = L^-1 S P[x,:]
+    ld* Ym = Wl + 40;    // 5 x 8: Y = Mi S P[x,:]
+    ld* Mm = Wl + 80;    // 5 x 5: Mi
+    for (int q = c.lane; q < 8 + NS; q += c.width) {   // column q of S P[x,:] (q < 8) or of I (q >= 8)
+      double v[NS];
+      for (int a = 0; a < NS; ++a) v[a] = (q < 8) ? S[a] * P8[a * 8 + q] : (a == q - 8 ? 1.0 : 0.0);
+      chol5_fwd(Lc, v);
+      if (q < 8)
+        for (int a = 0; a < NS; ++a) Wm[a * 8 + q] = v[a];
+      chol5_bwd(Lc, v);
+      for (int a = 0; a < NS; ++a) {
+        if (q < 8) Ym[a * 8 + q] = v[a];
+        else Mm[a * NS + (q - 8)] = v[a];
+      }
+    }
+    c.sync();
+    constexpr int PE = (64 + Ctx::width - 1) / Ctx::width;
+    double pn[PE];
+    {
+      int u = 0;
+      for (int e = c.lane; e < 64; e += c.width, ++u) {
+        const int r = e / 8, q = e % 8;
+        double v;
+        if (r < NS && q < NS) v = 0.5 * (Ym[r * 8 + q] / S[r] + Ym[q * 8 + r] / S[q]);
+        else if (r < NS) v = Ym[r * 8 + q] / S[r];
+        else if (q < NS) v = Ym[q * 8 + r] / S[q];
+        else {
+          v = P8[e];
+          for (int a = 0; a < NS; ++a) v -= Wm[a * 8 + r] * Wm[a * 8 + q];
+        }
+        pn[u] = v;
+      }
+    }
+    for (int e = c.lane; e < 2 * NS * NS; e += c.width) {
+      const int f = e < NS * NS ? e : e - NS * NS, a = f / NS, b = f % NS;
+      const double mi = 0.5 * (Mm[a * NS + b] + Mm[b * NS + a]);
+      Trec[e] = e < NS * NS ? S[a] * mi * S[b] : mi * S[b] / S[a];
+    }
+    c.sync();
+    {
+      int u = 0;
+      for (int e = c.lane; e < 64; e += c.width, ++u) P8[e] = pn[u];
+    }
+    c.sync();
+    return ok;
+  }
+  HTP_HD HTP_FI gd* trec(int i) const { return A(L.fac) + (int64_t)i * D.nb * D.nb; }
+  bool ric_relax = false;   // the current stage factor uses relaxed dynamics rows (T records valid)
+
+  // returns number of stages whose Rt is not positive definite
+  HTP_HD HTP_FI int riccati_factor(double dc) {
+    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
     ld* Pc = c.lds;          // 8x8 (stride 8): P_{i+1}
     ld* Pn = c.lds + 64;     // 8x8: P_i
     ld* Hw = c.lds + 128;    // 8x8 stage Hessian over w
@@ -2159,7 +2279,7 @@ struct ObcaSolver {
     ld* St = c.lds + 313;    // 3x8
     ld* AtPA = c.lds + 337;  // 5x5
     ld* Kl = c.lds + 362;    // 3x8
-    int bad = 0;
+    int bad = 0;             // relax_P scratch: c.lds + 240 .. 345 (PJx .. AtPA, dead between stages)
     // stage N-1: P = [[H_xx, 0], [0, 0]]
     {
       const gd* Kst = A(L.Kst) + (int64_t)(N - 1) * nb * nb;
@@ -2171,6 +2291,7 @@ struct ObcaSolver {
       c.sync();
       for (int e = c.lane; e < 64; e += c.width) Ps[e] = Pc[e];
     }
+    if (ric_relax && !relax_P(Pc, N - 1, dc, c.lds + 240, trec(N - 1))) ++bad;
     // stage records (H_w 64 | J 40 | C_{i-1} 6), prefetched one stage ahead
     ld* fb0 = c.lds + 400;
     ld* fb1 = c.lds + 512;
@@ -2279,6 +2400,7 @@ struct ObcaSolver {
       c.sync();
       for (int e = c.lane; e < 64; e += c.width) Pc[e] = 0.5 * (Pn[e] + Pn[(e % 8) * 8 + e / 8]);  // symmetrise
       c.sync();
+      if (ric_relax && !relax_P(Pc, i, dc, c.lds + 240, trec(i))) ++bad;
       HTP_PROF(5);
     }
     return bad;
@@ -2314,7 +2436,7 @@ struct ObcaSolver {
     return f.kind == 3 ? slot[f.off] : (f.kind == 4 ? 1.0 : 0.0);
   }
 
-  HTP_HD HTP_FI int riccati_factor_mfma() {
+  HTP_HD HTP_FI int riccati_factor_mfma(double dc) {
     const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
     const int64_t nb2 = (int64_t)nb * nb;
     const int col = c.lane & 15, rg = c.lane >> 4;
@@ -2359,6 +2481,21 @@ struct ObcaSolver {
       }
     }
     int bad = 0;
+    // relaxed rows: P_i goes through LDS (Pb) into relax_P and back into the C-layout registers
+    auto relax_regs = [&](int i) {
+      for (int r = 0; r < 2; ++r) {
+        const int row = rg + 4 * r;
+        if (col < 8) Pb[row * 8 + col] = Pc[r];
+      }
+      c.sync();
+      if (!relax_P(Pb, i, dc, c.lds + 112, trec(i))) ++bad;
+      for (int r = 0; r < 2; ++r) {
+        const int row = rg + 4 * r;
+        Pc[r] = (row < nz && col < nz) ? (double)Pb[row * 8 + col] : 0.0;
+      }
+      c.sync();
+    };
+    if (ric_relax) relax_regs(N - 1);
     double hcur[4], fcur[2], hnxt[4], fnxt[2];
     if (N >= 2) { ld_h(N - 2, hcur); ld_f(N - 2, fcur); }
     for (int i = N - 2; i >= 0; --i) {
@@ -2399,6 +2536,7 @@ struct ObcaSolver {
         Pc[r] = (r < 2 && row < nz && col < nz) ? 0.5 * (Pb[row * 8 + col] + Pb[col * 8 + row]) : 0.0;
       }
       c.sync();
+      if (ric_relax) relax_regs(i);
       for (int r = 0; r < 4; ++r) hcur[r] = hnxt[r];
       fcur[0] = fnxt[0];
       fcur[1] = fnxt[1];
@@ -2418,6 +2556,7 @@ struct ObcaSolver {
     const int N = D.N, nb = D.nb;
     const int64_t nb2 = (int64_t)nb * nb;
     const gd* LDa = A(L.LD);
+    const gd* Fa = A(L.fac);
     const int tot = cnt * RS_L;
     constexpr int U = ((RING_SB + 1) * RS_L + 63) / 64;
     double v[U];
@@ -2427,8 +2566,9 @@ struct ObcaSolver {
       const bool ok = e < tot && st < N;
       const int stc = ok ? st : 0;
       const gd* src = k < RS_SLOT ? LDa + (int64_t)stc * nb2 + k
-                    : (k < RS_X ? V + (int64_t)stc * nb + (k - RS_V) : X + (int64_t)stc * nb + (k - RS_X));
-      const bool in_blk = k < RS_SLOT || (k < RS_X ? k - RS_V < nb : k - RS_X < nb);
+                    : (k < RS_X ? V + (int64_t)stc * nb + (k - RS_V)
+                                : (k < RS_T ? X + (int64_t)stc * nb + (k - RS_X) : Fa + (int64_t)stc * nb2 + (k - RS_T)));
+      const bool in_blk = k < RS_SLOT || (k < RS_X ? k - RS_V < nb : (k < RS_T ? k - RS_X < nb : ric_relax));
       v[u] = (ok && in_blk) ? *src : 0.0;
     }
 #pragma unroll
@@ -2472,7 +2612,14 @@ struct ObcaSolver {
     }
     // stage-i record of the backward pass: -P_{i+1} (A, 2), F_i' (A, 2), K_i' (A, 1), [q_i; r_i] (C, 3),
     // e_{i+1} (B, 2, unscaled)
-    struct BRec { double mp[2], ft[2], kt, qr[3], e[2]; };
+    // T_i as the A operand of T r_x: lane supplies T[col][4 sgm + rg] (zero outside 5 x 5)
+    auto t_at = [&](const ld* slot, int sgm, int which) {   // which 0: T, 1: Q
+      const int k = rg + 4 * sgm;
+      return (col < NS && k < NS) ? (double)slot[RS_T + which * NS * NS + col * NS + k] : 0.0;
+    };
+    const bool rlx = ric_relax;
+    const dbl4 z4 = {0.0, 0.0, 0.0, 0.0};
+    struct BRec { double mp[2], ft[2], kt, qr[3], e[2], ta[2], qa[2]; };
     auto ld_b = [&](int i, BRec& R) {
       const ld* slot = rs(i);
       const ld* nslot = slot + RS_L;
@@ -2481,6 +2628,8 @@ struct ObcaSolver {
         R.ft[sgm] = f_at(fT[sgm], slot);
         const int row = rg + 4 * sgm;
         R.e[sgm] = (c0 && row < NS) ? nslot[RS_V + row] * nslot[SOFF + row] : 0.0;
+        R.ta[sgm] = rlx ? t_at(nslot, sgm, 0) : 0.0;
+        R.qa[sgm] = rlx ? t_at(nslot, sgm, 1) : 0.0;
       }
       R.kt = (rg < nv && col < nz) ? (double)slot[64 + rg * 8 + col] : 0.0;
       for (int r = 0; r < 3; ++r) {
@@ -2502,6 +2651,16 @@ struct ObcaSolver {
         if (i > lo) ld_b(i - 1, bn);
         dbl4 w = Ctx::mfma16(bc.mp[0], bc.e[0], pv);          // w = p - P e
         w = Ctx::mfma16(bc.mp[1], bc.e[1], w);
+        if (rlx) {                              // w_x = Q w_x, w_c -= P[c,x] T w_x (relax_P)
+          dbl4 t = Ctx::mfma16(bc.ta[0], w[0], z4);
+          t = Ctx::mfma16(bc.ta[1], w[1], t);
+          dbl4 q = Ctx::mfma16(bc.qa[0], w[0], z4);
+          q = Ctx::mfma16(bc.qa[1], w[1], q);
+          w = Ctx::mfma16(bc.mp[0], t[0], w);
+          w = Ctx::mfma16(bc.mp[1], t[1], w);
+          w[0] = q[0];                          // rows 0..3
+          if (rg == 0) w[1] = q[1];             // row 4
+        }
         dbl4 g = {bc.qr[0], bc.qr[1], bc.qr[2], 0.0};         // g = [q; r] + F' w
         g = Ctx::mfma16(bc.ft[0], w[0], g);
         g = Ctx::mfma16(bc.ft[1], w[1], g);
@@ -2526,7 +2685,7 @@ struct ObcaSolver {
     }
     // stage-i record of the forward pass: -P_i (A, 2), p_i (C, 2), K_i at rows V0.. (A, 2), F_i (A, 3),
     // e_{i+1} (C, 2), rt_i (3) + chol(Rt_i) (9), 1/sc of y_i (2)
-    struct FRec { double mp[2], p[2], ka[2], fa[3], e[2], rt[3], lc[9], isc[2]; };
+    struct FRec { double mp[2], p[2], ka[2], fa[3], e[2], rt[3], lc[9], isc[2], ta[2], qa[2]; };
     auto ld_f = [&](int i, FRec& R) {
       const ld* slot = rs(i);
       const ld* nslot = slot + RS_L;
@@ -2538,6 +2697,8 @@ struct ObcaSolver {
         R.ka[sgm] = (!last && col >= V0 && col < V0 + nv && k < nz) ? (double)slot[64 + (col - V0) * 8 + k] : 0.0;
         R.e[sgm] = (!last && c0 && row < NS) ? nslot[RS_V + row] * nslot[SOFF + row] : 0.0;
         R.isc[sgm] = (row < NS) ? (double)slot[SOFF + row] : 0.0;
+        R.ta[sgm] = rlx ? t_at(slot, sgm, 0) : 0.0;
+        R.qa[sgm] = rlx ? t_at(slot, sgm, 1) : 0.0;
       }
       for (int sgm = 0; sgm < 3; ++sgm) R.fa[sgm] = last ? 0.0 : f_at(fA[sgm], slot);
       for (int a = 0; a < 3; ++a) R.rt[a] = (!last && a < nv) ? (double)slot[RS_X + nz + a] : 0.0;
@@ -2555,6 +2716,16 @@ struct ObcaSolver {
         dbl4 y = {fc.p[0], fc.p[1], 0.0, 0.0};                 // y = p - P z
         y = Ctx::mfma16(fc.mp[0], zu[0], y);
         y = Ctx::mfma16(fc.mp[1], zu[1], y);
+        if (rlx) {                 // z = zh + T r_x, y = Q r_x (relax_P); zh was the nominal state
+          dbl4 t = Ctx::mfma16(fc.ta[0], y[0], z4);
+          t = Ctx::mfma16(fc.ta[1], y[1], t);
+          dbl4 q = Ctx::mfma16(fc.qa[0], y[0], z4);
+          q = Ctx::mfma16(fc.qa[1], y[1], q);
+          zu[0] += t[0];
+          zu[1] += t[1];
+          y[0] = q[0];
+          y[1] = q[1];
+        }
         gd* Xi = X + (int64_t)i * nb;
         const double zr0 = zu[0], zr1 = zu[1];
         for (int r = 0; r < 2; ++r) {
@@ -2695,6 +2866,28 @@ struct ObcaSolver {
         wv[r] = acc;
       }
       c.sync();
+      if (ric_relax) {  // w_x = Q_{i+1} w_x, w_c -= P[c,x] T_{i+1} w_x  (relax_P)
+        const gd* T = trec(i + 1);
+        constexpr int PN1 = (8 + Ctx::width - 1) / Ctx::width;
+        double wn[PN1];
+        int u = 0;
+        for (int r = c.lane; r < nz; r += c.width, ++u) {
+          double acc = r < NS ? 0.0 : wv[r];
+          for (int b = 0; b < NS; ++b) {
+            if (r < NS) acc += T[NS * NS + r * NS + b] * wv[b];
+            else {
+              double tb = 0.0;
+              for (int k = 0; k < NS; ++k) tb += T[b * NS + k] * wv[k];
+              acc -= cur[r * 5 + b] * tb;
+            }
+          }
+          wn[u] = acc;
+        }
+        c.sync();
+        u = 0;
+        for (int r = c.lane; r < nz; r += c.width, ++u) wv[r] = wn[u];
+        c.sync();
+      }
       for (int a2 = c.lane; a2 < nv; a2 += c.width) {  // rt = r + Jv' w + w_v
         double acc = cur[90 + a2] + wv[NS + a2];
         for (int t = 0; t < NS; ++t) acc += cur[40 + t * 8 + NS + a2] * wv[t];
@@ -2753,10 +2946,35 @@ struct ObcaSolver {
         const int e = c.lane + u * c.width;
         pre[u] = (i + 2 < N && e < RF) ? rec_get(dfw[u], i + 2, V, X) : 0.0;
       }
-      for (int k = c.lane; k < NS; k += c.width) {
-        double acc = cur[40 + k];
-        for (int t = 0; t < nz; ++t) acc -= cur[k * 8 + t] * zv[t];
-        yv[k] = acc * cur[129 + k];
+      if (ric_relax) {  // x_i = xh_i + T_i r_x, yh_i = Q_i r_x  with r = p - P zh (relax_P)
+        const gd* T = trec(i);
+        double rr[NS], tx[NS], qx[NS];
+        for (int k = 0; k < NS; ++k) {
+          double acc = cur[40 + k];
+          for (int t = 0; t < nz; ++t) acc -= cur[k * 8 + t] * zv[t];
+          rr[k] = acc;
+        }
+        for (int a = 0; a < NS; ++a) {
+          double at = 0.0, aq = 0.0;
+          for (int b = 0; b < NS; ++b) {
+            at += T[a * NS + b] * rr[b];
+            aq += T[NS * NS + a * NS + b] * rr[b];
+          }
+          tx[a] = at;
+          qx[a] = aq;
+        }
+        c.sync();
+        for (int k = c.lane; k < NS; k += c.width) {
+          yv[k] = qx[k] * cur[129 + k];
+          zv[k] += tx[k];
+        }
+        c.sync();
+      } else {
+        for (int k = c.lane; k < NS; k += c.width) {
+          double acc = cur[40 + k];
+          for (int t = 0; t < nz; ++t) acc -= cur[k * 8 + t] * zv[t];
+          yv[k] = acc * cur[129 + k];
+        }
       }
       if (i < N - 1) {
         double kv[3] = {cur[48], cur[49], cur[50]};
@@ -2843,14 +3061,19 @@ struct ObcaSolver {
     c.sync();
     long long t2 = c.clock();
     cyc[1] += t2 - t1;
-    // (the point formulation's hard terminal rows have no Riccati form: block LDL^T)
-    if (!PT && dc == 0.0 && !rs) {
+    // (the point formulation's hard terminal rows have no Riccati form: block LDL^T).  delta_c > 0 and
+    // the restoration phase relax the dynamics rows: the same recursion through relax_P.
+#ifndef HTP_RELAX_RICCATI
+#define HTP_RELAX_RICCATI 1   // 0: experiments only -- relaxed systems take the block LDL^T path (round 2)
+#endif
+    if (!PT && (HTP_RELAX_RICCATI || (dc == 0.0 && !rs))) {
       int bad;
+      ric_relax = dc != 0.0 || rs;
 #if defined(__HIPCC__)
-      if constexpr (Ctx::kMfma) bad = riccati_factor_mfma();
+      if constexpr (Ctx::kMfma) bad = riccati_factor_mfma(dc);
       else
 #endif
-        bad = riccati_factor();
+        bad = riccati_factor(dc);
       use_ric = true;
       cyc[2] += c.clock() - t2;
       neg_out = bad ? -1 : neg + NS * N + NS + D.md;

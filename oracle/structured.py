@@ -412,3 +412,128 @@ class StructuredKKT:
         dyd = (Jd @ dx - bd - bs / Ds) / Ed
         ds = (bs + dyd) / Ds
         return dx, ds, dyc, dyd
+
+
+class StructuredPointKKT:
+    """The augmented system of the point formulation (oracle/nlp_points.py, optimizer_points.py) by the
+    same eliminations: inequality slacks / multipliers, then the lambda-only local blocks of every
+    (obstacle j, step i) onto (x_i, y_i, theta_i) -- no equality rows, so each block is the positive
+    definite Hbar_zz -- then a block LDL^T over the N stage blocks plus one block for the hard
+    terminal rows X_{N-1} = end (coupled to x_{N-1}).  Inertia: unpivoted LDL^T pivots of the local
+    blocks when all are positive, Bunch-Kaufman otherwise; Bunch-Kaufman on every stage block."""
+
+    def __init__(self, nlp):
+        self.nlp = nlp
+        N = nlp.N
+        E = np.where(nlp.g_L == nlp.g_U)[0]
+        posE = -np.ones(nlp.m, dtype=int)
+        posE[E] = np.arange(E.size)
+        self.groups = []
+        for j in range(nlp.M):
+            sel = np.array([p for p, (jj, i, la0) in enumerate(nlp.blocks) if jj == j], dtype=int)
+            i = np.array([nlp.blocks[p][1] for p in sel], dtype=int)
+            la0 = np.array([nlp.blocks[p][2] for p in sel], dtype=int)
+            Z = la0[:, None] + np.arange(int(nlp.eo[j]))
+            Pv = np.stack([NS * i, NS * i + 1, NS * i + 3], axis=1)
+            self.groups.append(dict(stage=i, Z=Z, P=Pv))
+        self.stage_vars, self.stage_rows = [], []
+        for i in range(N):
+            v = list(NS * i + np.arange(NS))
+            if i < N - 1:
+                v += [nlp.oU + NC * i, nlp.oU + NC * i + 1]
+            rows = np.arange(NS) if i == 0 else nlp.gDyn + NS * (i - 1) + np.arange(NS)
+            self.stage_vars.append(np.array(v))
+            self.stage_rows.append(posE[rows])
+        self.stage_vars.append(np.zeros(0, dtype=int))                    # terminal block: rows only
+        self.stage_rows.append(posE[nlp.gTerm + np.arange(NS)])
+
+    def factor(self, Wm, Sx, Ss, Jc, Jd, dw, dc):
+        import scipy.sparse as sp
+        nlp = self.nlp
+        Wm, Jc, Jd = Wm.tocsr(), Jc.tocsr(), Jd.tocsr()
+        mc, md = Jc.shape[0], Jd.shape[0]
+        dcv = np.broadcast_to(np.asarray(dc, dtype=float), (mc + md,))
+        dcc, dcd = dcv[:mc], dcv[mc:]
+        Ds = Ss + dw
+        Ed = 1.0 / Ds + dcd
+        Hb = (Wm + sp.diags(Sx + dw) + Jd.T @ sp.diags(1.0 / Ed) @ Jd).tocsr()
+        self._Jd, self._Ds, self._Ed = Jd, Ds, Ed
+        pos, neg, zer = md, md, 0
+        N = nlp.N
+        schur = np.zeros((N, 3, 3))
+        self.gfac = []
+        for g in self.groups:
+            Z, Pv = g["Z"], g["P"]
+            K = _gather(Hb, Z[:, :, None], Z[:, None, :])
+            Bm = _gather(Hb, Z[:, :, None], Pv[:, None, :])
+            d = _ldl_nopiv(K)
+            ok = np.all(d > 0, axis=1) & np.all(np.isfinite(d), axis=1)
+            pos += int(np.sum(d[ok] > 0))
+            for b in np.where(~ok)[0]:
+                a, b_, c_ = _eig_inertia(K[b])
+                pos, neg, zer = pos + a, neg + b_, zer + c_
+            if zer:
+                return pos, neg, zer
+            KiB = np.linalg.solve(K, Bm)
+            np.add.at(schur, g["stage"], np.einsum("bki,bkj->bij", Bm, KiB))
+            self.gfac.append((K, Bm, KiB))
+        self.D, self.Lo = [], []
+        prev = None
+        sidx = np.array([0, 1, 3])
+        for i in range(N + 1):
+            v, r = self.stage_vars[i], self.stage_rows[i]
+            nv, nr = v.size, r.size
+            K = np.zeros((nr + nv, nr + nv))
+            K[:nr, :nr] = -np.diag(dcc[r])
+            Jr = _gather(Jc, r[:, None], v[None, :])
+            K[:nr, nr:] = Jr
+            K[nr:, :nr] = Jr.T
+            K[nr:, nr:] = _gather(Hb, v[:, None], v[None, :])
+            if i < N:
+                K[np.ix_(nr + sidx, nr + sidx)] -= schur[i]
+            if prev is not None:
+                pv, pr, Dp = prev
+                Off = np.zeros((nr + nv, pr.size + pv.size))
+                Off[:nr, pr.size:] = _gather(Jc, r[:, None], pv[None, :])
+                Off[nr:, pr.size:] = _gather(Hb, v[:, None], pv[None, :])
+                LD = np.linalg.solve(Dp, Off.T).T
+                K = K - LD @ Off.T
+                self.Lo.append((Off, LD))
+            a, b_, c_ = _eig_inertia(K)
+            pos, neg, zer = pos + a, neg + b_, zer + c_
+            self.D.append(K)
+            prev = (v, r, K)
+        return pos, neg, zer
+
+    def solve(self, bx, bs, bc, bd):
+        nlp = self.nlp
+        Jd, Ds, Ed = self._Jd, self._Ds, self._Ed
+        bxb = bx + Jd.T @ ((bd + bs / Ds) / Ed)
+        srhs = np.zeros(nlp.n)
+        kibs = []
+        for g, (K, Bm, KiB) in zip(self.groups, self.gfac):
+            Kib = np.linalg.solve(K, bxb[g["Z"]][:, :, None])[:, :, 0]
+            kibs.append(Kib)
+            np.add.at(srhs, g["P"], np.einsum("bkj,bk->bj", Bm, Kib))
+        nb = len(self.D)
+        V = []
+        for i in range(nb):
+            v, r = self.stage_vars[i], self.stage_rows[i]
+            rv = np.concatenate([bc[r], bxb[v] - srhs[v]])
+            V.append(rv if i == 0 else rv - self.Lo[i - 1][1] @ V[i - 1])
+        X = [None] * nb
+        X[nb - 1] = np.linalg.solve(self.D[nb - 1], V[nb - 1])
+        for i in range(nb - 2, -1, -1):
+            Off, LD = self.Lo[i]
+            X[i] = np.linalg.solve(self.D[i], V[i] - Off.T @ X[i + 1])
+        dx = np.zeros(nlp.n)
+        dyc = np.zeros(bc.size)
+        for i in range(nb):
+            v, r = self.stage_vars[i], self.stage_rows[i]
+            dyc[r] = X[i][:r.size]
+            dx[v] = X[i][r.size:]
+        for g, (K, Bm, KiB), Kib in zip(self.groups, self.gfac, kibs):
+            dx[g["Z"]] = Kib - np.einsum("bij,bj->bi", KiB, dx[g["P"]])
+        dyd = (Jd @ dx - bd - bs / Ds) / Ed
+        ds = (bs + dyd) / Ds
+        return dx, ds, dyc, dyd

@@ -117,10 +117,17 @@ def test_full_config_properties(ctx, cfg, nprob, min_ok):
     """Configs at their turn types (A fish-tail, B circle-back, C mixed with the mower)."""
     insts = [synth.config_instance(cfg, pid) for pid in range(nprob)]
     pk = _native.PackedBatch(insts)
-    res = ctx.solve(pk)
+    # config E (N=160, 12 obstacles, pruner): pids 6 and 10 run >2000 orig/restoration iterations
+    # into a local infeasibility / max_iter (pinned against the oracle in tests/golden/obca_full);
+    # here they run under the reference's default max_cpu_time (optimizer.py:475) to bound the test
+    ctx.set_option("max_cpu_time", 20.0 if cfg == "E" else 0.0)
+    try:
+        res = ctx.solve(pk)
+        solo = ctx.solve(_native.PackedBatch([insts[5]]))
+        again = ctx.solve(pk)
+    finally:
+        ctx.set_option("max_cpu_time", 0.0)
     ok = np.isin(res.status, [0, 1])
-    # config E (N=160, 12 obstacles, pruner) keeps a few long orig/restoration cycles that end at
-    # max_iter or in a local infeasibility (the oracle shows the same: oracle/ipm.py, DESIGN.md 3.1c)
     assert ok.mean() >= min_ok, np.bincount(res.status)
     for k in np.where(ok)[0][:6]:
         nlp = ObcaNLP(insts[k])
@@ -129,11 +136,10 @@ def test_full_config_properties(ctx, cfg, nprob, min_ok):
         if cfg != "E":
             assert _stationarity(nlp, res.x[k]) <= 1e-5, k
     # batch-composition invariance: problem 5 alone == problem 5 inside the batch
-    solo = ctx.solve(_native.PackedBatch([insts[5]]))
     assert np.array_equal(solo.x[0], res.x[5])
-    # determinism
-    again = ctx.solve(pk)
-    assert np.array_equal(again.x, res.x)
+    # determinism (problems stopped by the wall-clock limit excepted)
+    det = res.status != 6
+    assert np.array_equal(again.x[det], res.x[det])
 
 
 def test_max_cpu_time_stops_the_solve(ctx):
