@@ -292,7 +292,10 @@ HTP_HD inline void bk_solve_packed(T* K, const int* ip, int n, double* v) {
 
 // LDS ring of the matrix-core Riccati passes (ObcaSolver::ring_fill): RING_SB + 1 stage records of
 // RS_L doubles (LD slot prefix [0, SOFF + NS), V_i, X_i) after the per-wave scratch and filter.
-constexpr int RING_SB = 8;                       // stages per block
+#ifndef HTP_RING_SB
+#define HTP_RING_SB 8
+#endif
+constexpr int RING_SB = HTP_RING_SB;             // stages per block
 constexpr int RS_SLOT = 142;                     // LD slot prefix (P | K | chol | J | 1/sc)
 constexpr int RS_V = RS_SLOT, RS_X = RS_SLOT + NBMAX;
 constexpr int RS_T = RS_SLOT + 2 * NBMAX;        // T_i, Q_i of the relaxed dynamics rows (relax_P), 5 x 5 each
@@ -301,7 +304,10 @@ constexpr int RING_OFF = 4 * NBMAX * NBMAX + 8 + 2 * 64;
 constexpr int RING_DOUBLES = (RING_SB + 1) * RS_L;
 // pivoted local blocks (ObcaSolver::local_pivoted) on the device: one packed 10x10 block per lane in LDS,
 // over the same region as the ring (never live at the same time)
-constexpr int PIV_LDS_PER_LANE = 55;
+#ifndef HTP_PIV_LDS
+#define HTP_PIV_LDS 1   // 0: pivoted blocks in private memory (smaller LDS footprint; experiments)
+#endif
+constexpr int PIV_LDS_PER_LANE = HTP_PIV_LDS ? 55 : 0;
 constexpr int LDS_WAVE_DOUBLES = RING_OFF + (RING_DOUBLES > 64 * PIV_LDS_PER_LANE ? RING_DOUBLES : 64 * PIV_LDS_PER_LANE);
 
 // ---------------------------------------------------------------------------
@@ -1180,7 +1186,7 @@ struct ObcaSolver {
     // Device, 4-edge blocks: dsytf2 on this lane's LDS slice instead of a runtime-indexed private
     // array (every update a scratch read-modify-write).  Free here: the slice overlaps only the
     // Riccati ring, which no local sweep uses.  Same arithmetic, bit-identical.
-    if constexpr (Ctx::kMfma && NPK <= PIV_LDS_PER_LANE) {
+    if constexpr (Ctx::kMfma && HTP_PIV_LDS && NPK <= PIV_LDS_PER_LANE) {
       ld* K = c.lds + RING_OFF + c.lane * NPK;
       for (int q = 0; q < NPK; ++q) K[q] = B.K[q];
       bk_factor_packed(K, ip, NL, inertia[0], inertia[1]);
@@ -3488,6 +3494,13 @@ struct ObcaSolver {
   }
 
   // original-problem theta at (x, s) during the restoration phase: c = c_R - n + p, d = d_R - n_d + p_d
+  HTP_HD HTP_FI double orig_inf_max_rs(const gd* cc, const gd* dd, const gd* s, const gd* R) const {
+    const int mc = D.mc, md = D.md;
+    double t = 0;
+    for (int r = c.lane; r < mc; r += c.width) t = dmax(t, dabs(cc[r] - R[r] + R[mc + r]));
+    for (int r = c.lane; r < md; r += c.width) t = dmax(t, dabs(dd[r] - R[2 * mc + r] + R[2 * mc + md + r] - s[r]));
+    return c.maxv(t);
+  }
   HTP_HD HTP_FI double orig_theta_rs(const gd* cc, const gd* dd, const gd* s, const gd* R) const {
     const int mc = D.mc, md = D.md;
     double t = 0;
@@ -4497,7 +4510,9 @@ struct ObcaSolver {
           continue;  // the original problem resumes with this iteration number
         }
         if (!rs_first && (optimal || (acc_lvl && ls_.acc_count + 1 >= o.acceptable_iter))) {
-          const double ot = orig_theta_rs(cc, dd, s, A(L.R));
+          // RestoConvergenceCheck: max-norm primal infeasibility of the original problem <= 1e2 tol ->
+          // "Restoration_Failed" (converged to a feasible point the filter rejects), else locally infeasible
+          const double ot = orig_inf_max_rs(cc, dd, s, A(L.R));
           status = ot <= 1e2 * o.tol ? ST_RESTORATION : ST_INFEASIBLE;
           if (have_acc) { copy_arr(x, A(L.ax), D.n); status = ST_ACCEPTABLE; }
           break;

@@ -676,7 +676,9 @@ class _Ipm:
             if p.is_resto:
                 if not first and (optimal or (accept_lvl and self.acc_count + 1 >= o["acceptable_iter"])):
                     # the restoration problem converged without reaching an acceptable original point
-                    ot = self.parent.orig_theta(it.x[:p.nx], it.s)
+                    # RestoConvergenceCheck: orig_ip_cq->trial_primal_infeasibility(NORM_MAX) <= 1e2 tol
+                    # -> RESTORATION_CONVERGED_TO_FEASIBLE_POINT, else LOCALLY_INFEASIBLE
+                    ot = self.parent.orig_primal_inf_max(it.x[:p.nx], it.s)
                     self.parent_status = RESTO_FAILED if ot <= 1e2 * o["tol"] else INFEASIBLE
                     raise _Stop(self.parent_status)
                 self.acc_count = self.acc_count + 1 if accept_lvl else 0
@@ -1003,6 +1005,11 @@ class _Ipm:
     def orig_theta(self, x, s):
         c, d = self.p.cd(x)
         return self.theta(c, d, s)
+
+    def orig_primal_inf_max(self, x, s):
+        """Max-norm primal infeasibility of the (scaled) original problem at (x, s)."""
+        c, d = self.p.cd(x)
+        return max(np.max(np.abs(c), initial=0.0), np.max(np.abs(d - s), initial=0.0))
 
     def restoration(self, it, ref):
         """MinC_1NrmRestorationPhase::PerformRestoration (original problem only)."""

@@ -3,10 +3,14 @@ the C ABI: the HIP kernel against the solver core's host build (same
 algorithm; device libm differs from glibc in the last bits, so iterates agree
 to ~1e-9, not bitwise) and against the oracle IPM on small cases; the shim end
 to end.  Tolerance: states within 1e-6 of the oracle (north_star: 1e-4)."""
+import glob
+import os
+
 import numpy as np
 import pytest
 
 import _hostsim as H
+from _fixture_io import load_instance
 from headland_trajectory_planning_amd import _native, geometry, synth
 from headland_trajectory_planning_amd.obca_py.car_model_obca import CarModel
 from headland_trajectory_planning_amd.obca_py import optimizer_points as OP
@@ -105,3 +109,25 @@ def test_shim_end_to_end(ctx):
     assert np.max(np.abs(np.asarray(opt.x_opt).ravel() - X[:, 0])) < 1e-6
     assert np.max(np.abs(np.asarray(opt.theta_opt).ravel() - X[:, 3])) < 1e-6
     assert len(opt.a_opt.elements()) == 11 and opt.steer_opt.full().shape == (12, 1)
+
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "points_full")
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "P*.npz"))),
+                         ids=lambda p: os.path.basename(p)[:-4])
+def test_full_size_parity_vs_oracle_fixtures(ctx, path):
+    """N = 80, 6 obstacles (the tools/bench_points.py instances) against oracle fixtures
+    (tests/golden/make_points_golden.py, structured-KKT oracle, max_cpu_time off), including
+    problems the oracle ends infeasible: same status; states <= 1e-4 and objective <= 1e-6 rel
+    when converged."""
+    g = np.load(path)
+    N = int(g["N"])
+    inst = load_instance(g)
+    res = ctx.solve_points(_native.PointsPackedBatch([inst]))
+    st = int(g["status"])
+    assert res.status[0] == st, (int(res.status[0]), st, int(res.iterations[0]), int(g["iters"]))
+    assert (res.n_resto[0] > 0) == (int(g["n_resto"]) > 0)
+    if st in (0, 1):
+        assert np.max(np.abs(res.x[0, :5 * N] - g["states"])) <= 1e-4
+        assert abs(res.objective[0] - float(g["f"])) <= 1e-6 * max(1.0, abs(float(g["f"])))
