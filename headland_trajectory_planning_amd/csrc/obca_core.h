@@ -3031,6 +3031,72 @@ struct ObcaSolver {
     HTP_PROF(7);
   }
 
+  // ---------------------------------------------- point formulation: hard terminal rows
+  // optimizer_points.py:273-278 adds X_{N-1} = end as equality rows (stage-chain block N):
+  //   K Z + C' y_T = r_Z,  C Z - E_T y_T = r_T,   C Z = s_T o x_{N-1},  E_T = dc (+ e_R in restoration).
+  // With K the stage chain (Riccati), the terminal multipliers solve the 5 x 5 system
+  //   (S_T Sig S_T + E_T) y_T = s_T o (K^-1 r_Z)_x - r_T,   Sig = K^-1 [x_{N-1}, x_{N-1}],
+  // then Z = K^-1 (r_Z - C' y_T).  Inertia (Sylvester, Schur on y_T): the 5 terminal negatives iff
+  // S_T Sig S_T + E_T is positive definite.  Sig = five solves with unit right-hand sides at x_{N-1}.
+  HTP_HD HTP_FI void ric_solve(const gd* V, gd* X) {
+#if defined(__HIPCC__)
+    if constexpr (Ctx::kMfma) { riccati_solve_mfma(V, X); return; }
+#endif
+    riccati_solve(V, X);
+  }
+  // chol(S_T Sig S_T + E_T) (15, reciprocal pivots) and s_T (5) into fac slot N; false if not pos. def.
+  HTP_HD HTP_FI bool terminal_schur(double dc) {
+    const int N = D.N, nb = D.nb;
+    gd* V = A(L.V);
+    gd* X = A(L.X);
+    gd* rec = A(L.fac) + (int64_t)N * nb * nb;
+    const gd* scE = A(L.scE);
+    const gd* eR = A(L.eR);
+    for (int k = 0; k < NS; ++k) {
+      for (int e = c.lane; e < N * nb; e += c.width) V[e] = (e == (N - 1) * nb + NS + k) ? 1.0 : 0.0;
+      c.sync();
+      ric_solve(V, X);
+      c.sync();
+      for (int j = c.lane; j < NS; j += c.width) rec[20 + k * NS + j] = X[(int64_t)(N - 1) * nb + NS + j];
+      c.sync();
+    }
+    double Sm[NS * NS], Lc[15], sT[NS];
+    for (int k = 0; k < NS; ++k) sT[k] = scE[D.eTerm + k];
+    for (int a = 0; a < NS; ++a)
+      for (int b = 0; b < NS; ++b) {
+        const double sig = 0.5 * (rec[20 + a * NS + b] + rec[20 + b * NS + a]);
+        Sm[a * NS + b] = sT[a] * sig * sT[b] + (a == b ? dc + (rs ? eR[D.eTerm + a] : 0.0) : 0.0);
+      }
+    const bool ok = chol5(Sm, Lc);
+    c.sync();
+    for (int e = c.lane; e < 20; e += c.width) rec[e] = e < 15 ? Lc[e] : sT[e - 15];
+    c.sync();
+    return ok;
+  }
+  // the stage-chain solve with the terminal rows: V (blocks 0..N-1, block N = r_T) -> X (block N = y_T)
+  HTP_HD HTP_FI void ric_solve_terminal(gd* V, gd* X) {
+    const int N = D.N, nb = D.nb;
+    const gd* rec = A(L.fac) + (int64_t)N * nb * nb;
+    ric_solve(V, X);
+    c.sync();
+    double Lc[15], sT[NS], y[NS];
+    for (int e = 0; e < 15; ++e) Lc[e] = rec[e];
+    for (int k = 0; k < NS; ++k) {
+      sT[k] = rec[15 + k];
+      y[k] = sT[k] * X[(int64_t)(N - 1) * nb + NS + k] - V[(int64_t)N * nb + k];
+    }
+    chol5_fwd(Lc, y);
+    chol5_bwd(Lc, y);
+    c.sync();
+    for (int k = c.lane; k < NS; k += c.width) {
+      V[(int64_t)(N - 1) * nb + NS + k] -= sT[k] * y[k];
+      X[(int64_t)N * nb + k] = y[k];
+    }
+    c.sync();
+    ric_solve(V, X);
+    c.sync();
+  }
+
   // ---------------------------------------------------------- factorization
   // returns true if the inertia is the one IPOPT requires
   HTP_HD HTP_PHASE void factorize(bool ls, double dw, double dc, int& neg_out, int& zero_out) {
@@ -3067,12 +3133,16 @@ struct ObcaSolver {
     c.sync();
     long long t2 = c.clock();
     cyc[1] += t2 - t1;
-    // (the point formulation's hard terminal rows have no Riccati form: block LDL^T).  delta_c > 0 and
-    // the restoration phase relax the dynamics rows: the same recursion through relax_P.
+    // delta_c > 0 and the restoration phase relax the dynamics rows: the same recursion through
+    // relax_P.  The point formulation's hard terminal rows (block N) enter through their 5 x 5 Schur
+    // complement (terminal_schur).
 #ifndef HTP_RELAX_RICCATI
 #define HTP_RELAX_RICCATI 1   // 0: experiments only -- relaxed systems take the block LDL^T path (round 2)
 #endif
-    if (!PT && (HTP_RELAX_RICCATI || (dc == 0.0 && !rs))) {
+#ifndef HTP_PT_RICCATI
+#define HTP_PT_RICCATI 1      // 0: experiments only -- the point formulation takes the block LDL^T path
+#endif
+    if ((!PT || HTP_PT_RICCATI) && (HTP_RELAX_RICCATI || (dc == 0.0 && !rs))) {
       int bad;
       ric_relax = dc != 0.0 || rs;
 #if defined(__HIPCC__)
@@ -3081,10 +3151,20 @@ struct ObcaSolver {
 #endif
         bad = riccati_factor(dc);
       use_ric = true;
-      cyc[2] += c.clock() - t2;
-      neg_out = bad ? -1 : neg + NS * N + NS + D.md;
-      zero_out = zero;
-      return;
+      bool done = true;
+      if constexpr (PT) {
+        // Riccati pivots and the terminal Schur complement all positive definite => exact inertia.
+        // Otherwise the chain without its terminal rows may still be indefinite on directions the
+        // terminal rows remove: the block LDL^T below decides (the reference's exact inertia).
+        if (!bad && !terminal_schur(dc)) bad = 1;
+        done = bad == 0;
+      }
+      if (done) {
+        cyc[2] += c.clock() - t2;
+        neg_out = bad ? -1 : neg + NS * N + NS + D.md;
+        zero_out = zero;
+        return;
+      }
     }
     use_ric = false;
     // sequential block LDL^T over stages, in LDS:
@@ -3219,11 +3299,8 @@ struct ObcaSolver {
     c.sync();
     gd* X = A(L.X);
     if (use_ric) {
-#if defined(__HIPCC__)
-      if constexpr (Ctx::kMfma) riccati_solve_mfma(V, X);
-      else
-#endif
-        riccati_solve(V, X);
+      if constexpr (PT) ric_solve_terminal(V, X);
+      else ric_solve(V, X);
     } else {
     // forward: V_i -= LD_i V_{i-1}
     for (int i = 1; i < D.nblk; ++i) {

