@@ -2551,6 +2551,138 @@ struct ObcaSolver {
     return bad;
   }
 
+  // Sig = K^-1 [x_{N-1}, x_{N-1}] of the stage chain (point formulation's terminal rows, terminal_schur):
+  // the two Riccati passes with the five unit right-hand sides at x_{N-1} carried as columns 0..4 of the
+  // 16-wide MFMA tiles (the single-vector passes use column 0 only), so one pass costs the MFMAs of one
+  // solve.  The right-hand side is zero outside x_{N-1}: backward p_{N-1} = [I; 0], w = p (e = 0);
+  // forward z_0 = 0.  Per-stage p_i (8 x 5) and rt_i (3 x 5) go to the fac slot after relax_P's T / Q.
+  // Records are read straight from HBM one stage ahead.  Result: sig[5 x 5] (global).
+  HTP_HD HTP_FI void riccati_sigma_mfma(gd* sig) {
+    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
+    const int64_t nb2 = (int64_t)nb * nb;
+    const int col = c.lane & 15, rg = c.lane >> 4;
+    const bool cw = col < NS;                 // a right-hand-side column
+    const gd* LDa = A(L.LD);
+    gd* Fa = A(L.fac);
+    constexpr int PO = 50, RO = 90;           // p_i [8][5] and rt_i [3][5] in fac slot i
+    FSrc fT[2], fA[3];
+    for (int sgm = 0; sgm < 2; ++sgm) fT[sgm] = f_src(rg + 4 * sgm, col);
+    for (int sgm = 0; sgm < 3; ++sgm) fA[sgm] = f_src(col, rg + 4 * sgm);
+    auto p_at = [&](const gd* slot, int sgm) {
+      const int k = rg + 4 * sgm;
+      return (col < nz && k < nz) ? (double)slot[col * 8 + k] : 0.0;
+    };
+    auto t_at = [&](const gd* tr, int sgm, int which) {
+      const int k = rg + 4 * sgm;
+      return (col < NS && k < NS) ? (double)tr[which * NS * NS + col * NS + k] : 0.0;
+    };
+    const bool rlx = ric_relax;
+    const dbl4 z4 = {0.0, 0.0, 0.0, 0.0};
+    // ---------------- backward: p_{N-1} = [I_5; 0] (columns 0..4)
+    dbl4 pv = z4;
+    for (int r = 0; r < 2; ++r) {
+      const int row = rg + 4 * r;
+      pv[r] = (cw && row == col) ? 1.0 : 0.0;
+    }
+    auto st_p = [&](int i, const dbl4& v) {
+      gd* d = Fa + (int64_t)i * nb2 + PO;
+      for (int r = 0; r < 2; ++r) {
+        const int row = rg + 4 * r;
+        if (cw && row < 8) d[row * NS + col] = v[r];
+      }
+    };
+    st_p(N - 1, pv);
+    struct BR { double mp[2], ft[2], kt, ta[2], qa[2]; };
+    auto ld_b = [&](int i, BR& R) {
+      const gd* slot = LDa + (int64_t)i * nb2;
+      const gd* nslot = slot + nb2;
+      const gd* tr = Fa + (int64_t)(i + 1) * nb2;
+      for (int sgm = 0; sgm < 2; ++sgm) {
+        R.mp[sgm] = -p_at(nslot, sgm);
+        R.ft[sgm] = f_get(fT[sgm], slot);
+        R.ta[sgm] = rlx ? t_at(tr, sgm, 0) : 0.0;
+        R.qa[sgm] = rlx ? t_at(tr, sgm, 1) : 0.0;
+      }
+      R.kt = (rg < nv && col < nz) ? (double)slot[64 + rg * 8 + col] : 0.0;
+    };
+    BR bc, bn;
+    if (N >= 2) ld_b(N - 2, bc);
+    for (int i = N - 2; i >= 0; --i) {
+      if (i > 0) ld_b(i - 1, bn);
+      dbl4 w = pv;                                   // w = p - P e, e = 0
+      if (rlx) {
+        dbl4 t = Ctx::mfma16(bc.ta[0], w[0], z4);
+        t = Ctx::mfma16(bc.ta[1], w[1], t);
+        dbl4 q = Ctx::mfma16(bc.qa[0], w[0], z4);
+        q = Ctx::mfma16(bc.qa[1], w[1], q);
+        w = Ctx::mfma16(bc.mp[0], t[0], w);
+        w = Ctx::mfma16(bc.mp[1], t[1], w);
+        w[0] = q[0];
+        if (rg == 0) w[1] = q[1];
+      }
+      dbl4 g = z4;                                   // g = F' w ([q; r] = 0)
+      g = Ctx::mfma16(bc.ft[0], w[0], g);
+      g = Ctx::mfma16(bc.ft[1], w[1], g);
+      pv = Ctx::mfma16(bc.kt, g[2], g);              // p = g_z + K' rt
+      st_p(i, pv);
+      gd* rt = Fa + (int64_t)i * nb2 + RO;
+      if (cw && rg < nv) rt[rg * NS + col] = g[2];
+      bc = bn;
+    }
+    c.sync();
+    // ---------------- forward: z_0 = 0
+    dbl4 zu = z4;
+    struct FR { double mp[2], p[2], ka[2], fa[3], rt[3], lc[9], ta[2], qa[2]; };
+    auto ld_f = [&](int i, FR& R) {
+      const gd* slot = LDa + (int64_t)i * nb2;
+      const gd* fs = Fa + (int64_t)i * nb2;
+      const bool last = i >= N - 1;
+      for (int sgm = 0; sgm < 2; ++sgm) {
+        const int row = rg + 4 * sgm, k = rg + 4 * sgm;
+        R.mp[sgm] = rlx ? -p_at(slot, sgm) : 0.0;
+        R.p[sgm] = (rlx && cw && row < nz) ? (double)fs[PO + row * NS + col] : 0.0;
+        R.ka[sgm] = (!last && col >= V0 && col < V0 + nv && k < nz) ? (double)slot[64 + (col - V0) * 8 + k] : 0.0;
+        R.ta[sgm] = rlx ? t_at(fs, sgm, 0) : 0.0;
+        R.qa[sgm] = rlx ? t_at(fs, sgm, 1) : 0.0;
+      }
+      for (int sgm = 0; sgm < 3; ++sgm) R.fa[sgm] = last ? 0.0 : f_get(fA[sgm], slot);
+      for (int a = 0; a < 3; ++a) R.rt[a] = (!last && cw && a < nv) ? (double)fs[RO + a * NS + col] : 0.0;
+      for (int k = 0; k < 9; ++k) R.lc[k] = last ? 0.0 : (double)slot[88 + k];
+    };
+    FR fc, fn;
+    ld_f(0, fc);
+    for (int i = 0; i < N; ++i) {
+      if (i < N - 1) ld_f(i + 1, fn);
+      if (rlx) {                                     // z = zh + T r_x,  r = p - P zh
+        dbl4 y = {fc.p[0], fc.p[1], 0.0, 0.0};
+        y = Ctx::mfma16(fc.mp[0], zu[0], y);
+        y = Ctx::mfma16(fc.mp[1], zu[1], y);
+        dbl4 t = Ctx::mfma16(fc.ta[0], y[0], z4);
+        t = Ctx::mfma16(fc.ta[1], y[1], t);
+        zu[0] += t[0];
+        zu[1] += t[1];
+      }
+      if (i < N - 1) {
+        double kv[3] = {fc.rt[0], fc.rt[1], fc.rt[2]};
+        chol3_solve(fc.lc, nv, kv);
+        dbl4 u = {zu[0], zu[1], (cw && rg < nv) ? kv[rg] : 0.0, 0.0};
+        u = Ctx::mfma16(fc.ka[0], zu[0], u);
+        u = Ctx::mfma16(fc.ka[1], zu[1], u);
+        dbl4 zn = z4;                                // z_{i+1} = F u (e = 0)
+        zn = Ctx::mfma16(fc.fa[0], u[0], zn);
+        zn = Ctx::mfma16(fc.fa[1], u[1], zn);
+        zn = Ctx::mfma16(fc.fa[2], u[2], zn);
+        zu = zn;
+      }
+      fc = fn;
+    }
+    for (int r = 0; r < 2; ++r) {                    // x_{N-1}: rows 0..4 of z, columns 0..4
+      const int row = rg + 4 * r;
+      if (cw && row < NS) sig[row * NS + col] = zu[r];
+    }
+    c.sync();
+  }
+
   // V (block order [y|x|u|tau]) -> X (same order), the two passes on the matrix core.
   // Stage data reach the passes through an LDS ring of RING_SB + 1 stage records (the LD slot's
   // P | K | chol(Rt) | J | 1/sc prefix, V_i, X_i): one cooperative, coalesced global -> LDS copy
@@ -3052,13 +3184,20 @@ struct ObcaSolver {
     gd* rec = A(L.fac) + (int64_t)N * nb * nb;
     const gd* scE = A(L.scE);
     const gd* eR = A(L.eR);
-    for (int k = 0; k < NS; ++k) {
-      for (int e = c.lane; e < N * nb; e += c.width) V[e] = (e == (N - 1) * nb + NS + k) ? 1.0 : 0.0;
-      c.sync();
-      ric_solve(V, X);
-      c.sync();
-      for (int j = c.lane; j < NS; j += c.width) rec[20 + k * NS + j] = X[(int64_t)(N - 1) * nb + NS + j];
-      c.sync();
+#if defined(__HIPCC__)
+    if constexpr (Ctx::kMfma) {
+      riccati_sigma_mfma(rec + 20);       // all five columns in one pair of passes
+    } else
+#endif
+    {
+      for (int k = 0; k < NS; ++k) {
+        for (int e = c.lane; e < N * nb; e += c.width) V[e] = (e == (N - 1) * nb + NS + k) ? 1.0 : 0.0;
+        c.sync();
+        ric_solve(V, X);
+        c.sync();
+        for (int j = c.lane; j < NS; j += c.width) rec[20 + k * NS + j] = X[(int64_t)(N - 1) * nb + NS + j];
+        c.sync();
+      }
     }
     double Sm[NS * NS], Lc[15], sT[NS];
     for (int k = 0; k < NS; ++k) sT[k] = scE[D.eTerm + k];

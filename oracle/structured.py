@@ -151,7 +151,10 @@ class StructuredKKTLoop:
                 Off = np.zeros((nr + nv, pr.size + pv.size))
                 Off[:nr, pr.size:] = jsub(r, pv)
                 Off[nr:, pr.size:] = hsub(v, pv)
-                LD = np.linalg.solve(Dp, Off.T).T
+                try:
+                    LD = np.linalg.solve(Dp, Off.T).T
+                except np.linalg.LinAlgError:   # exactly singular previous block: reported as singular
+                    return pos, neg, zer + 1
                 K = K - LD @ Off.T
                 self.Lo.append((Off, LD))
             a, b_, c_ = _eig_inertia(K)
@@ -361,7 +364,10 @@ class StructuredKKT:
                 Off = np.zeros((nr + nv, pr.size + pv.size))
                 Off[:nr, pr.size:] = _gather(Jc, r[:, None], pv[None, :])
                 Off[nr:, pr.size:] = _gather(Hb, v[:, None], pv[None, :])
-                LD = np.linalg.solve(Dp, Off.T).T
+                try:
+                    LD = np.linalg.solve(Dp, Off.T).T
+                except np.linalg.LinAlgError:   # exactly singular previous block: reported as singular
+                    return pos, neg, zer + 1
                 K = K - LD @ Off.T
                 self.Lo.append((Off, LD))
             a, b_, c_ = _eig_inertia(K)
@@ -500,7 +506,10 @@ class StructuredPointKKT:
                 Off = np.zeros((nr + nv, pr.size + pv.size))
                 Off[:nr, pr.size:] = _gather(Jc, r[:, None], pv[None, :])
                 Off[nr:, pr.size:] = _gather(Hb, v[:, None], pv[None, :])
-                LD = np.linalg.solve(Dp, Off.T).T
+                try:
+                    LD = np.linalg.solve(Dp, Off.T).T
+                except np.linalg.LinAlgError:   # exactly singular previous block: reported as singular
+                    return pos, neg, zer + 1
                 K = K - LD @ Off.T
                 self.Lo.append((Off, LD))
             a, b_, c_ = _eig_inertia(K)

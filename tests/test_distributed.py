@@ -154,3 +154,35 @@ def test_two_rank_work_stealing_solve_matches_single_process():
         assert np.array_equal(out[rk][3], ref.x[ids])     # the union equals a one-process solve, bit for bit
         assert np.array_equal(out[rk][4], ref.status[ids])
         assert np.array_equal(out[rk][5], ref.iterations[ids])
+
+
+# ------------------------------------------------- bench.py's multi-rank instance path
+def _bench_gen_worker(rank, world, port, out):
+    """bench.py's order: generate this rank's slice (fork pool, before any torch/GPU init), publish it
+    to /dev/shm, then bring up the process group and assemble the global batch from every slice."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import bench
+    own = bench.generate_own_slice(12, "D", rank, world, procs=2)
+    bench.publish_slice(own, rank)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pk = bench.assemble_global_batch(own, rank, world, dist)
+    out[rank] = (pk.batch, float(pk.traj.sum()), float(pk.obs_A.sum()), float(np.nansum(np.where(np.isfinite(pk.params), pk.params, 0.0))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_instances_generated_before_the_process_group_and_assembled():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    world, port = 2, _free_port()
+    out = mp.Manager().dict()
+    mp.spawn(_bench_gen_worker, args=(world, port, out), nprocs=world, join=True)
+    solo = bench.generate_own_slice(12, "D", 0, 1, procs=1)
+    ref = (solo.batch, float(solo.traj.sum()), float(solo.obs_A.sum()), float(np.nansum(np.where(np.isfinite(solo.params), solo.params, 0.0))))
+    assert out[0] == ref and out[1] == ref        # every rank holds the whole global batch, in pid order
