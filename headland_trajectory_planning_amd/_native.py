@@ -89,7 +89,8 @@ EXPORTS = ["htp_obca_sizes", "htp_create", "htp_destroy", "htp_last_error", "htp
            "htp_obca_points_sizes", "htp_obca_points_solve_batch", "htp_obca_points_solve_batch_device",
            "htp_init_ref_path_batch", "htp_init_ref_path_batch_device", "htp_init_ref_path_last_ms",
            "htp_queue_create", "htp_queue_destroy", "htp_queue_publish", "htp_queue_close", "htp_queue_published",
-           "htp_queue_claimed", "htp_obca_solve_queue_device", "htp_obca_resident_waves"]
+           "htp_queue_claimed", "htp_obca_solve_queue_device", "htp_obca_resident_waves",
+           "htp_oge_obstacles_batch", "htp_oge_obstacles_batch_device", "htp_oge_last_ms"]
 
 
 def _declare(lib):
@@ -166,6 +167,13 @@ def _declare(lib):
     lib.htp_obca_solve_queue_device.restype = ctypes.c_int
     lib.htp_obca_resident_waves.argtypes = [ctypes.c_void_p, ctypes.POINTER(ObcaBatch)]
     lib.htp_obca_resident_waves.restype = ctypes.c_int32
+    lib.htp_oge_obstacles_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(OgeBatch), ctypes.POINTER(OgeResult)]
+    lib.htp_oge_obstacles_batch.restype = ctypes.c_int
+    lib.htp_oge_obstacles_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(OgeBatch),
+                                                   ctypes.POINTER(OgeResult), ctypes.c_void_p]
+    lib.htp_oge_obstacles_batch_device.restype = ctypes.c_int
+    lib.htp_oge_last_ms.argtypes = [ctypes.c_void_p]
+    lib.htp_oge_last_ms.restype = ctypes.c_double
     return lib
 
 
@@ -629,6 +637,80 @@ class YparkResults:
         return r
 
 
+# ------------------------------------------------------- orchard scene -> OBCA obstacles (htp_oge.hip)
+OGE_NPARAM, OGE_MAXROWS, OGE_MAXPOLY, OGE_MAXV = 16, 32, 32, 12
+OGE_STATUS = {0: "ok", 1: "bad_input", 2: "no_row_between", 3: "overflow", 4: "empty_side"}
+
+
+class OgeBatch(ctypes.Structure):  # htp_oge_batch
+    _fields_ = [("batch", ctypes.c_int32), ("max_rows", ctypes.c_int32), ("params", ctypes.c_void_p),
+                ("row_draws", ctypes.c_void_p), ("eps_draws", ctypes.c_void_p)]
+
+
+class OgeResult(ctypes.Structure):  # htp_oge_result
+    _fields_ = [("status", ctypes.c_void_p), ("n_poly", ctypes.c_void_p), ("n_vert", ctypes.c_void_p),
+                ("vertices", ctypes.c_void_p), ("n_facet", ctypes.c_void_p), ("A", ctypes.c_void_p),
+                ("b", ctypes.c_void_p)]
+
+
+class OgePacked:
+    """Scenes for htp_oge_obstacles_batch.  A scene is a dict with nrows, row_width, row_length, slope,
+    tree_width, headland_width, start, end, side (1 NEAR / -1 FAR) and the reference's random draws:
+    row_draws (create_tree_rows, one per row) and eps_draws (create_headland_countour_lines, one per row)."""
+
+    def __init__(self, scenes):
+        B = len(scenes)
+        self.batch = B
+        self.max_rows = max(3, max((int(s["nrows"]) for s in scenes), default=3))
+        if self.max_rows > OGE_MAXROWS:
+            raise ValueError(f"[oge] at most {OGE_MAXROWS} tree rows per scene")
+        self.params = np.zeros((B, OGE_NPARAM))
+        self.row_draws = np.zeros((B, self.max_rows))
+        self.eps_draws = np.zeros((B, self.max_rows))
+        for b, s in enumerate(scenes):
+            n = int(s["nrows"])
+            self.params[b, :13] = [n, s["row_width"], s["row_length"], s["slope"], s["tree_width"],
+                                   s["headland_width"], *np.asarray(s["start"], dtype=np.float64)[:3],
+                                   *np.asarray(s["end"], dtype=np.float64)[:3], s.get("side", 1)]
+            self.row_draws[b, :n] = s["row_draws"]
+            self.eps_draws[b, :n] = s["eps_draws"]
+
+    def struct(self, ptrs=None):
+        p = ptrs or {}
+        return OgeBatch(self.batch, self.max_rows, p.get("params", self.params.ctypes.data),
+                        p.get("row_draws", self.row_draws.ctypes.data), p.get("eps_draws", self.eps_draws.ctypes.data))
+
+
+class OgeResults:
+    def __init__(self, batch, halfspaces=True):
+        B = batch
+        self.status = np.zeros(B, np.int32)
+        self.n_poly = np.zeros(B, np.int32)
+        self.n_vert = np.zeros((B, OGE_MAXPOLY), np.int32)
+        self.vertices = np.zeros((B, OGE_MAXPOLY, OGE_MAXV, 2))
+        self.n_facet = np.zeros((B, OGE_MAXPOLY), np.int32) if halfspaces else None
+        self.A = np.zeros((B, OGE_MAXPOLY, OGE_MAXV, 2)) if halfspaces else None
+        self.b = np.zeros((B, OGE_MAXPOLY, OGE_MAXV)) if halfspaces else None
+
+    def struct(self):
+        def ptr(a):
+            return None if a is None else a.ctypes.data
+        return OgeResult(self.status.ctypes.data, self.n_poly.ctypes.data, self.n_vert.ctypes.data,
+                         self.vertices.ctypes.data, ptr(self.n_facet), ptr(self.A), ptr(self.b))
+
+    def polygons(self, b):
+        """Scene b's obstacle polygons [(n_v, 2) arrays] in the reference's order."""
+        return [self.vertices[b, q, :self.n_vert[b, q]].copy() for q in range(int(self.n_poly[b]))]
+
+    def halfspaces(self, b):
+        """Scene b's [(A, b)] (compute_polytope_halfspaces of each polygon)."""
+        out = []
+        for q in range(int(self.n_poly[b])):
+            f = int(self.n_facet[b, q])
+            out.append((self.A[b, q, :f].copy(), self.b[b, q, :f].copy()))
+        return out
+
+
 class WorkQueue:
     """Host work queue of problem indices feeding one persistent solve launch
     (htp_queue_*: pinned, GPU-coherent host memory)."""
@@ -699,6 +781,17 @@ class Context:
         if rc != 0:
             raise RuntimeError(f"[htp] htp_obca_points_solve_batch failed: {self.error()}")
         return res
+
+    def oge_obstacles(self, packed, halfspaces=True):
+        """Batched orchard scene -> OBCA obstacle polygons (+ halfspaces), host buffers -> OgeResults."""
+        r = OgeResults(packed.batch, halfspaces)
+        b, rs = packed.struct(), r.struct()
+        if self.lib.htp_oge_obstacles_batch(self.ctx, ctypes.byref(b), ctypes.byref(rs)) != 0:
+            raise RuntimeError(f"[htp] htp_oge_obstacles_batch failed: {self.error()}")
+        return r
+
+    def oge_last_ms(self):
+        return self.lib.htp_oge_last_ms(self.ctx)
 
     def init_ref_path(self, packed):
         """Batched get_init_ref_path (host buffers) -> RefPathResults."""

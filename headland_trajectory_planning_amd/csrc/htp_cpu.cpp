@@ -55,3 +55,15 @@ extern "C" int htp_cpu_obca_solve_range(const htp_obca_batch* in, htp_obca_resul
   }
   return 0;
 }
+
+// Reeds-Shepp words for one pose pair on the host (rs_core.h, the same core as htp_rs_all_paths_batch).
+// Used by the workload generator's fish-tail warm starts (synth.py), which run before any GPU call.
+#include "rs_host.h"
+
+extern "C" int htp_cpu_rs_all_paths(const double* q, int64_t cap_paths, int64_t cap_points, int32_t* n_paths,
+                                    int64_t* n_points, double* lengths, int8_t* ctypes, double* L,
+                                    int64_t* point_offsets, double* x, double* y, double* yaw, double* cs,
+                                    int8_t* dir) {
+  return htp::rs::all_paths_host(q, cap_paths, cap_points, n_paths, n_points, lengths, ctypes, L, point_offsets, x, y,
+                                 yaw, cs, dir);
+}

@@ -37,6 +37,8 @@ struct htp_ctx {
   void* rp_ws = nullptr;
   size_t rp_ws_bytes = 0;
   hipEvent_t rp_ev0 = nullptr, rp_ev1 = nullptr;
+  // orchard scene -> OBCA obstacles (htp_oge.hip)
+  hipEvent_t oge_ev0 = nullptr, oge_ev1 = nullptr;
 };
 
 static inline int fail(htp_ctx* c, const std::string& m) {

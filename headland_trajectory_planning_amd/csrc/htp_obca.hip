@@ -179,6 +179,8 @@ htp_ctx* htp_create(int32_t device) {
   (void)hipEventCreate(&c->yp_ev1);
   (void)hipEventCreate(&c->rp_ev0);
   (void)hipEventCreate(&c->rp_ev1);
+  (void)hipEventCreate(&c->oge_ev0);
+  (void)hipEventCreate(&c->oge_ev1);
   return c;
 }
 
@@ -202,6 +204,8 @@ void htp_destroy(htp_ctx* c) {
   if (c->rp_ws) (void)hipFree(c->rp_ws);
   if (c->rp_ev0) (void)hipEventDestroy(c->rp_ev0);
   if (c->rp_ev1) (void)hipEventDestroy(c->rp_ev1);
+  if (c->oge_ev0) (void)hipEventDestroy(c->oge_ev0);
+  if (c->oge_ev1) (void)hipEventDestroy(c->oge_ev1);
   delete c;
 }
 

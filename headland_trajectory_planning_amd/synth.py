@@ -3,33 +3,27 @@
 Problem `pid` is drawn from Philox(key=[20251015, pid]) so a problem is
 identical for any batch composition and any GPU count.
 
-Geometry follows the reference's orchard model:
-* tree rows  ........... R/path_planner/utils/map_utils.py:45-61 (create_tree_rows)
-* exit / enter poses ... map_utils.py:228-271 (get_base_pose, NEAR_SIDE)
-* obstacles ............ R/path_planner/OGE_OBCA.py:306-373,477-677: a headland
-  boundary quad, the up/low bound quad and tree-row rectangles (SAFETY_BOUND 0.2),
-  trimmed / padded to exactly M convex quads (padding: far dummy quads, >= 50 m away)
-* warm start ........... one of the reference's turn types (`turn=`):
-  - "dubins": the Dubins fallback (R/path_planner/OBCA_warm_start.py:166-174,
-    pydubins shortest path);
-  - "circleback": the circle-back / Omega turn of
-    R/path_planner/safety_forward_path_plan.py:395-454 (forward arc R_f by
-    theta, reverse arc R_b by pi - theta, Dubins lead-in; radii grow 5 % until
-    the reverse arc ends short of the row; rows wider than 2R fall back to Dubins);
-  - "fishtail": a three-arc C|C|C K-turn (forward, reverse, forward at the
-    minimum radius, symmetric outer arcs) joined to the row poses by straights --
-    the Reeds-Shepp C|C|C family the fish-tail planner
-    (safety_forward_path_plan.py:300-392) picks between offset poses of one x;
-    rows wider than 2R fall back to Dubins;
+Two scene builders:
+
+* `config_instance` / `make_orchard_instance` -- the BASELINE configs A-E.  The
+  scene and the warm start come from the reference's own producers, restated in
+  path_planner/ (see the block comment above make_orchard_instance): tree rows
+  (map_utils.create_tree_rows), row poses (get_base_pose), the Dubins /
+  circle-back / fish-tail planners of safety_forward_path_plan.py and
+  OBCA_warm_start.py, get_init_ref_path, and OGE_OBCA's obstacle producer
+  (create_boundary_polygons, get_obstacle_tree_rows, get_obstacles_for_OBCA).
+* `make_instance` -- hand-placed rectangle scenes (headland boundary quad, the
+  up bound quad, tree-row rectangles, far dummy quads) with closed-form
+  warm starts; small-shape parity tests and the smoke test use it:
+  - "dubins": the shortest Dubins word (pydubins);
+  - "circleback": forward arc R_f by theta, reverse arc R_b by pi - theta,
+    Dubins lead-in (safety_forward_path_plan.py:395-454);
+  - "fishtail": a three-arc C|C|C K-turn at the minimum radius joined to the
+    row poses by straights;
   - "mixed": one of the three per problem (its own Philox stream, key + 1).
   The path is sampled to exactly N poses and turned into [x, y, v, theta, steer]
-  as R/obca_py/util.py:62-113 does (v = dir*desired_v, steer = atan(L*kappa)
-  with kappa the steering curvature, v[0]=v[-1]=steer[0]=0, heading wrapped +
-  unwrapped).
-
-The headland boundary is placed behind the warm start's swept footprint with a
-random margin, so every instance starts collision-free and the boundary is
-close to active -- the regime the reference notebooks exercise.
+  as R/obca_py/util.py:62-113 does; the boundary sits behind the warm start's
+  swept footprint with a random margin.
 """
 import math
 
@@ -406,14 +400,341 @@ def make_points_instance(pid, N=80, M=6, implement="none", key=20251015, **over)
     return inst
 
 
+# ------------------------------------------------ the reference's own scene producers
+# Configs A-E are built by the reference's planners and obstacle producer (restated in
+# path_planner/), not by the hand-placed rectangles of make_instance:
+#   tree rows ........ map_utils.create_tree_rows (R/path_planner/utils/map_utils.py:45-61)
+#   row poses ........ get_base_pose (map_utils.py:228-271), NEAR side
+#   warm start ....... dubins:     get_warm_start_path_dubins (R/path_planner/OBCA_warm_start.py:166-174)
+#                      circleback: get_circle_back_path_full (R/path_planner/safety_forward_path_plan.py:395-454)
+#                      fishtail:   get_start_end_pose_for_reeds_shepp (:300-364) + the Reeds-Shepp word with the
+#                                  least backward length among the collision-free ones + Dubins lead-in/out
+#                                  (R/test/classic_planner.ipynb cells 10-11)
+#   init guess ....... get_init_ref_path (R/obca_py/util.py:62-113) at desired_v = ds / dT, resampled to N rows
+#   obstacles ........ orchard_environment_OBCA.create_boundary_polygons / get_obstacle_tree_rows /
+#                      get_obstacles_for_OBCA (R/path_planner/OGE_OBCA.py:306-373,477-677)
+# The reference's global np.random draws (create_tree_rows :33, create_headland_countour_lines
+# orchard_geometry_environment.py:71) come from an MT19937 stream seeded per problem from its Philox
+# stream, so a problem is identical for any batch composition and any GPU count.
+_CPU_LIB = None
+SAFETY_BOUND = 0.2   # orchard_environment_OBCA.SAFETY_BOUND: the row rectangles' margin past the row ends
+
+
+def _cpu_lib():
+    global _CPU_LIB
+    if _CPU_LIB is None:
+        import ctypes
+        import os
+        so = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhtp_cpu.so")
+        lib = ctypes.CDLL(so)
+        f = lib.htp_cpu_rs_all_paths
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 11
+        _CPU_LIB = lib
+    return _CPU_LIB
+
+
+class _RSPath:
+    __slots__ = ("lengths", "ctypes", "L", "x", "y", "yaw", "cs", "directions")
+
+
+def host_rs_all_paths(sx, sy, syaw, gx, gy, gyaw, maxc, step_size):
+    """calc_all_paths (R/path_planner/utils/reeds_shepp.py:39-65) on the host through the CPU build of
+    csrc/rs_core.h (libhtp_cpu.so) -- the generator runs before the GPU is touched."""
+    import ctypes  # noqa: F401
+    f = _cpu_lib().htp_cpu_rs_all_paths
+    q = np.array([sx, sy, syaw, gx, gy, gyaw, maxc, step_size], dtype=np.float64)
+    n_p, n_q = np.zeros(1, np.int32), np.zeros(1, np.int64)
+    cp, cq = 48, 4096
+    for _ in range(2):
+        ln, ct, L = np.zeros((cp, 5)), np.zeros((cp, 5), np.int8), np.zeros(cp)
+        off = np.zeros(cp + 1, np.int64)
+        x, y, yaw, cs = (np.zeros(cq) for _ in range(4))
+        d = np.zeros(cq, np.int8)
+        st = f(q.ctypes.data, cp, cq, n_p.ctypes.data, n_q.ctypes.data, ln.ctypes.data, ct.ctypes.data,
+               L.ctypes.data, off.ctypes.data, x.ctypes.data, y.ctypes.data, yaw.ctypes.data, cs.ctypes.data,
+               d.ctypes.data)
+        if cp >= n_p[0] and cq >= n_q[0]:
+            break
+        cp, cq = int(n_p[0]), int(n_q[0])
+    if st != 0:
+        raise ValueError("[synth] Reeds-Shepp sampler status %d" % st)
+    out = []
+    for k in range(int(n_p[0])):
+        p = _RSPath()
+        nseg = int(np.count_nonzero(ct[k] != 3))
+        a, b = int(off[k]), int(off[k + 1])
+        p.lengths, p.ctypes, p.L = ln[k, :nseg].copy(), ["LSR-"[t] for t in ct[k, :nseg]], float(L[k])
+        p.x, p.y, p.yaw, p.cs, p.directions = x[a:b].copy(), y[a:b].copy(), yaw[a:b].copy(), cs[a:b].copy(), \
+            d[a:b].astype(np.float64)
+        out.append(p)
+    return out
+
+
+class _legacy_random:
+    """Seed numpy's global MT19937 stream (the reference draws from np.random.*) and restore it after."""
+
+    def __init__(self, seed):
+        self.seed = int(seed)
+
+    def __enter__(self):
+        self.saved = np.random.get_state()
+        np.random.seed(self.seed)
+
+    def __exit__(self, *exc):
+        np.random.set_state(self.saved)
+        return False
+
+
+def _fishtail_path(tree_rows, s_row, e_row, car, empty, env, start, end, exit_off, enter_off):
+    """classic_planner.ipynb cells 10-11 (R/path_planner/safety_forward_path_plan.py:300-364 + the word
+    choice): rows [x, y, yaw, k, dir] or None when no Reeds-Shepp word clears the rows."""
+    from .path_planner import map_utils
+    from .path_planner import safety_forward_path_plan as sfp
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        safe_start, safe_end, leave_off, enter_off = sfp.get_start_end_pose_for_reeds_shepp(
+            tree_rows, s_row, e_row, car, env, max_steer_angle=0.55, side=map_utils.NEAR_SIDE,
+            extra_offset_enter_dist=enter_off, extra_offset_leave_dist=exit_off)
+    paths = host_rs_all_paths(safe_start[0], safe_start[1], safe_start[2], safe_end[0], safe_end[1], safe_end[2],
+                              car.curvature, 0.1)
+    optimal, best = None, 99999
+    for p in paths:
+        traj = np.array([p.x, p.y, p.yaw]).T
+        if env.check_path_feasibility(empty, traj, boundary_check=False):
+            lengths = np.array(p.lengths)
+            cost = np.abs(lengths[lengths < 0].sum())
+            if cost < best:
+                optimal, best = p, cost
+    if optimal is None:
+        return None
+    path = np.array([optimal.x, optimal.y, optimal.yaw, optimal.cs, optimal.directions]).T
+    r = 1.0 / car.curvature
+    if leave_off > 0.1:
+        path = np.vstack([sfp.get_dubins_path_full(start, safe_start, r)[:-1], path])
+    if enter_off > 0.1:
+        path = np.vstack([path, sfp.get_dubins_path_full(safe_end, end, r)[1:]])
+    return path
+
+
+def _warm_start_path(turn, tree_rows, s_row, e_row, car, empty, env, start, end, exit_off, enter_off):
+    from .path_planner import map_utils
+    from .path_planner import safety_forward_path_plan as sfp
+    r = 1.0 / car.curvature
+    if turn == "fishtail":
+        return _fishtail_path(tree_rows, s_row, e_row, car, empty, env, start, end, exit_off, enter_off)
+    if turn == "circleback":
+        return sfp.get_circle_back_path_full(start, end, r, car, side=map_utils.NEAR_SIDE, step_size=0.1)
+    return sfp.get_dubins_path_full(start, end, r, step_size=0.1)      # OBCA_warm_start.py:166-174
+
+
+def _resample_rows(ref, N):
+    """get_init_ref_path output (rows [x, y, v, theta, steer]) -> exactly N rows at even arc length
+    (x, y, theta, steer interpolated; v = the gear speed of the covering row; v[0] = v[-1] = steer[0] = 0)."""
+    seg = np.hypot(np.diff(ref[:, 0]), np.diff(ref[:, 1]))
+    s = np.concatenate([[0.0], np.cumsum(seg)])
+    t = np.linspace(0.0, s[-1], N)
+    out = np.zeros((N, 5))
+    for c in (0, 1, 3, 4):
+        out[:, c] = np.interp(t, s, ref[:, c])
+    idx = np.clip(np.searchsorted(s, t, side="right"), 1, len(s) - 1)
+    v = ref[idx, 2]
+    v = np.where(v == 0.0, ref[idx - 1, 2], v)
+    out[:, 2] = v
+    out[0, 2] = out[-1, 2] = 0.0
+    out[0, 4] = 0.0
+    return out
+
+
+def _split_quads(poly):
+    """A convex k-gon (k >= 5) as overlapping convex quads [v0, v_i, v_i+1, v_i+2] whose union is the
+    polygon: the OBCA distance constraint to each piece holds iff it holds to the union, so the
+    free space is unchanged while every obstacle slot of a batch keeps 4 edges."""
+    P = np.asarray(poly, dtype=np.float64)
+    if P.shape[0] <= 4:
+        return [P]
+    out, i = [], 1
+    while True:
+        j = min(i, P.shape[0] - 3)
+        out.append(np.vstack([P[0], P[j], P[j + 1], P[j + 2]]))
+        if j + 2 >= P.shape[0] - 1:
+            return out
+        i += 2
+
+
+def _needed_headland(tree_rows, pts, angle):
+    """Smallest headland_width whose field boundary (get_map_exterior_pts :288-334, near side) leaves
+    every point inside: boundary x(y) = near row end x(y) - width / |sin(angle)|."""
+    ys, xs = tree_rows[:, 0, 1], tree_rows[:, 0, 0]
+    o = np.argsort(ys)
+    xr = np.interp(pts[:, 1], ys[o], xs[o])
+    return float(np.max(xr - pts[:, 0])) * abs(math.sin(angle))
+
+
+def make_orchard_instance(pid, N=80, M=6, implement="none", key=20251015, turn="dubins", **over):
+    """One OBCA instance whose scene and warm start come from the reference's producers (see the block
+    comment above).  Draws per attempt: row width U[2.2, 3.5], slope U[-15, 15] deg, l_std in {0, 1},
+    start row 0..4, row jump 1..3 (1 for fish-tail / circle-back), leave offset U[-1, 1], enter offset
+    U[0, 3.66], boundary margin U[0.3, 1.0].  The headland is 6 m (the notebooks' value) or wider when the
+    warm start needs it (boundary = margin behind its footprint); an attempt is redrawn when the planner
+    finds no path, when its path fails the reference's footprint predicate against the tree rows
+    (check_path_feasibility, implements included), or when the OBCA init guess reaches deeper than the
+    rows' SAFETY_BOUND into an obstacle -- as in the reference, the warm start may start inside that
+    0.2 m margin, which OBCA (min_dist 0.1) then clears.  Obstacles: the
+    producer's list in its order (k-gons split into overlapping quads); with more than M the M closest to
+    the warm start are kept, with fewer the other tree rows of the orchard (nearest first) and the other
+    bound quad are added (far dummy quads only if the orchard has none left)."""
+    from .path_planner import map_utils
+    from .path_planner.car_model import CarModel
+    from .path_planner.OGE_OBCA import orchard_environment_OBCA
+    from .obca_py.util import get_init_ref_path
+
+    rng = np.random.Generator(np.random.Philox(key=[key, pid]))
+    if turn == "mixed":
+        turn = TURN_TYPES[int(np.random.Generator(np.random.Philox(key=[key + 1, pid])).integers(0, 3))]
+    if turn not in TURN_TYPES:
+        raise ValueError("unknown turn type %r" % (turn,))
+    veh = dict(VEHICLE)
+    feat = IMPLEMENTS[implement]
+    car = CarModel(max_steer=veh["max_steer"], wheel_base=veh["wheelbase"], axle_to_front=veh["axle_to_front"],
+                   axle_to_back=veh["axle_to_back"], width=veh["width"],
+                   aux_poly_features=[feat] if feat is not None else [], with_aux=feat is not None)
+    empty = CarModel(max_steer=veh["max_steer"], wheel_base=veh["wheelbase"], axle_to_front=veh["axle_to_front"],
+                     axle_to_back=veh["axle_to_back"], width=veh["width"], with_aux=False)
+    polys = [geometry.body_rectangle(veh["axle_to_front"], veh["axle_to_back"], veh["width"])]
+    if feat is not None:
+        polys.append(geometry.implement_rectangle(feat))
+    dT = float(over.get("dT", DEFAULT_WEIGHTS["dT"]))
+    rows_n, row_len, tree_w = max(8, M), 20.0, 0.3   # 8 rows (SURVEY 8(d)); more when M asks for more obstacles
+    cand = None
+    for _attempt in range(64):
+        row_w = rng.uniform(2.2, 3.5)
+        slope = math.radians(rng.uniform(-15.0, 15.0))
+        l_std = [0.0, 1.0][int(rng.integers(0, 2))]
+        s_row = int(rng.integers(0, 5))
+        e_row = min(s_row + int(rng.integers(1, 4)), rows_n - 2)
+        if turn != "dubins":
+            e_row = s_row + 1
+        exit_off = rng.uniform(-1.0, 1.0)
+        enter_off = rng.uniform(0.0, 3.66)
+        margin = rng.uniform(0.3, 1.0)
+        seed = int(rng.integers(0, 2 ** 31 - 1))
+        with _legacy_random(seed):
+            tree_rows = map_utils.create_tree_rows(rows_n, row_w, row_len, slope_angle=slope, l_std=l_std)
+        start = map_utils.get_base_pose(s_row, tree_rows, exit_off, side=map_utils.NEAR_SIDE,
+                                        pose_type=map_utils.LEAVE_POSE)
+        end = map_utils.get_base_pose(e_row, tree_rows, enter_off, side=map_utils.NEAR_SIDE,
+                                      pose_type=map_utils.ENTER_POSE)
+        env = orchard_environment_OBCA(tree_rows, [], tree_width=tree_w, headland_width=6.0)
+        try:
+            path = _warm_start_path(turn, tree_rows, s_row, e_row, car, empty, env, start, end, exit_off, enter_off)
+        except (ValueError, IndexError, ZeroDivisionError):
+            path = None
+        if path is None or len(path) < 4:
+            continue
+        # the reference's own footprint predicate on the whole warm start (tree rows, implements included;
+        # orchard_geometry_environment.py:423-458): a planner output that fails it is redrawn
+        if not env.check_path_feasibility(car, path[:, :3], boundary_check=False, aux_check=True):
+            continue
+        Lp = float(np.sum(np.hypot(np.diff(path[:, 0]), np.diff(path[:, 1]))))
+        ds = Lp / (N - 1)
+        desired_v = min(ds / dT, 0.9)
+        try:
+            ref = get_init_ref_path(car, path[:, 0], path[:, 1], path[:, 2], path[:, 3], path[:, 4],
+                                    desired_v=desired_v, ds=ds / 2.0)
+        except ValueError:
+            continue
+        traj = _resample_rows(ref, N)
+        poses = np.stack([traj[:, 0], traj[:, 1], traj[:, 3]], axis=1)
+        dense = np.stack([ref[:, 0], ref[:, 1], ref[:, 3]], axis=1)
+        foot = [_polys_at(p, np.vstack([poses, dense])) for p in polys]
+        pts = np.concatenate([f.reshape(-1, 2) for f in foot])
+        hw = max(6.0, _needed_headland(tree_rows, pts, env.get_headland_angle(env.NEAR_SIDE)) + margin)
+        env = orchard_environment_OBCA(tree_rows, [], tree_width=tree_w, headland_width=hw)
+        with _legacy_random(seed + 1):
+            boundary = env.create_boundary_polygons()
+        row_polys = env.get_obstacle_tree_rows(start, end)
+        obs = env.get_obstacles_for_OBCA(boundary, row_polys, start, end, side=env.NEAR_SIDE)
+        pool = [q for o in obs for q in _split_quads(o)]
+        if len(pool) < M:   # the rest of the orchard: other tree rows (nearest first), the other bound quad
+            used_rows = {round(float(np.mean(np.asarray(p)[:, 1])), 6) for p in row_polys}
+            mid = 0.5 * (start[1] + end[1])
+            extra = sorted((abs(r[0, 1] - mid), i) for i, r in enumerate(tree_rows)
+                           if round(float(r[0, 1]), 6) not in used_rows)
+            pool += [env._row_rect(tree_rows[i], False) for _, i in extra]
+            pool += [p for p in (boundary[3] if start[1] > end[1] else boundary[2])]
+        gaps = np.array([min(_min_sat_gap(f, q) for f in foot) for q in pool])
+        if np.any(gaps <= -SAFETY_BOUND):   # deeper than the rows' SAFETY_BOUND margin (OGE_OBCA.py:411-475)
+            continue
+        if len(pool) > M:
+            keep = sorted(np.argsort(gaps, kind="stable")[:M])
+            pool = [pool[k] for k in keep]
+        cand = pool
+        break
+    if cand is None:
+        raise RuntimeError("[synth] problem %d: no collision-free warm start in 64 attempts" % pid)
+    k = 0
+    while len(cand) < M:  # far dummy quads (only when the orchard has no obstacle left)
+        cx = start[0] + 60.0 + 5.0 * k
+        cand.append(_rect(cx, cx + 1.0, start[1] + 60.0, start[1] + 61.0))
+        k += 1
+    obs_A, obs_b = zip(*[geometry.polytope_halfspaces(o) for o in cand])
+    body_G, body_g = zip(*[geometry.polytope_halfspaces(p) for p in polys])
+    inst = dict(
+        init_traj=traj, obs_A=list(obs_A), obs_b=list(obs_b), body_G=list(body_G), body_g=list(body_g),
+        obstacles=cand, dT=dT, Q=DEFAULT_WEIGHTS["Q"].copy(), R=DEFAULT_WEIGHTS["R"].copy(),
+        W=DEFAULT_WEIGHTS["W"].copy(), wheelbase=veh["wheelbase"], max_steer=veh["max_steer"],
+        max_velocity=1.0, max_accel=1.0, max_steer_rate=0.7, min_dist=0.1,
+        x_bound=[-np.inf, np.inf], y_bound=[-np.inf, np.inf],
+        meta=dict(pid=pid, turn=turn, length=Lp, start=tuple(start), goal=tuple(end), s_row=s_row, e_row=e_row,
+                  headland_width=hw, n_producer=len(obs), n_dummy=k, l_std=l_std, nrows=rows_n, row_width=row_w,
+                  row_length=row_len, slope=slope, tree_width=tree_w, seed=seed),
+    )
+    for kk, vv in over.items():
+        inst[kk] = vv
+    return inst
+
+
+def orchard_scene(meta):
+    """The scene of a make_orchard_instance problem as the device producer takes it (htp_oge_obstacles_batch,
+    _native.OgePacked): geometry plus the reference's np.random draws, regenerated from the problem's MT19937
+    seeds (create_tree_rows: one uniform(-l_std, l_std) per row under `seed`; create_headland_countour_lines:
+    uniform(-0.5, 0.5, size=rows) under `seed + 1`)."""
+    n = int(meta["nrows"])
+    with _legacy_random(meta["seed"]):
+        row_draws = np.array([np.random.uniform(-meta["l_std"], meta["l_std"]) for _ in range(n)])
+    with _legacy_random(meta["seed"] + 1):
+        eps_draws = np.random.uniform(-0.5, 0.5, size=(n,))
+    return dict(nrows=n, row_width=meta["row_width"], row_length=meta["row_length"], slope=meta["slope"],
+                tree_width=meta["tree_width"], headland_width=meta["headland_width"], start=meta["start"],
+                end=meta["goal"], side=1, row_draws=row_draws, eps_draws=eps_draws)
+
+
+def orchard_obstacles_host(meta):
+    """The reference producer's obstacle list for the same scene, through the Python restatement
+    (orchard_environment_OBCA); the device producer is pinned against it."""
+    from .path_planner import map_utils
+    from .path_planner.OGE_OBCA import orchard_environment_OBCA
+    with _legacy_random(meta["seed"]):
+        rows = map_utils.create_tree_rows(int(meta["nrows"]), meta["row_width"], meta["row_length"],
+                                          slope_angle=meta["slope"], l_std=meta["l_std"])
+    env = orchard_environment_OBCA(rows, [], tree_width=meta["tree_width"], headland_width=meta["headland_width"])
+    with _legacy_random(meta["seed"] + 1):
+        boundary = env.create_boundary_polygons()
+    row_polys = env.get_obstacle_tree_rows(meta["start"], meta["goal"])
+    return env.get_obstacles_for_OBCA(boundary, row_polys, meta["start"], meta["goal"], side=env.NEAR_SIDE)
+
+
 # turn types of the BASELINE configs: A fish-tail, B Omega/circle-back, C mixed, D/E the Dubins turn
 TURNS = {"A": "fishtail", "B": "circleback", "C": "mixed", "D": "dubins", "E": "dubins"}
 
 
 def config_instance(cfg, pid, **over):
-    """Problem `pid` of BASELINE config `cfg` (shape, implement and turn type)."""
+    """Problem `pid` of BASELINE config `cfg` (shape, implement and turn type), scene and warm start from
+    the reference's producers (make_orchard_instance)."""
     _, N, M, imp = CONFIGS[cfg]
-    return make_instance(pid, N=N, M=M, implement=imp, turn=TURNS[cfg], **over)
+    return make_orchard_instance(pid, N=N, M=M, implement=imp, turn=TURNS[cfg], **over)
 
 
 CONFIGS = {

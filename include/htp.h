@@ -358,6 +358,52 @@ int htp_ypark_search_batch(htp_ctx* ctx, const htp_ypark_batch* in, htp_ypark_re
 int htp_ypark_search_batch_device(htp_ctx* ctx, const htp_ypark_batch* in, htp_ypark_result* out, void* stream);
 double htp_ypark_last_ms(htp_ctx* ctx);
 
+/* ---------------------------------------------------------------------------
+ * Orchard scene -> OBCA obstacles: the synthetic orchard
+ * of R/path_planner/utils/map_utils.py create_tree_rows :45-61 and the OGE_OBCA
+ * obstacle producer, one scene per GPU thread (csrc/oge_core.h):
+ *   env = orchard_environment_OBCA(tree_rows, [], tree_width, headland_width)
+ *   boundary = env.create_boundary_polygons()          OGE_OBCA.py:306-373
+ *   rows = env.get_obstacle_tree_rows(start, end)      :477-591
+ *   obstacles = env.get_obstacles_for_OBCA(boundary, rows, start, end, side)  :593-677
+ * and, per obstacle, compute_polytope_halfspaces as R/obca_py/optimizer.py:184-186
+ * calls it (A x <= b, cdd row normalisation, 7-decimal rounding).  The reference's
+ * np.random draws are inputs (row_draws: create_tree_rows' uniform(-l_std, l_std)
+ * per row; eps_draws: create_headland_countour_lines' uniform(-0.5, 0.5) per row,
+ * orchard_geometry_environment.py:71).  Polygons come out in the reference's order. */
+#define HTP_OGE_NPARAM 16
+enum {
+  HTP_OGE_P_NROWS = 0,   /* tree rows (3..32) */
+  HTP_OGE_P_ROWW, HTP_OGE_P_ROWLEN, HTP_OGE_P_SLOPE,   /* create_tree_rows row_width, row_lengths, slope_angle */
+  HTP_OGE_P_TREEW, HTP_OGE_P_HW,                       /* tree_width, headland_width */
+  HTP_OGE_P_SX, HTP_OGE_P_SY, HTP_OGE_P_SYAW,          /* start (row-leave) pose */
+  HTP_OGE_P_EX, HTP_OGE_P_EY, HTP_OGE_P_EYAW,          /* end (row-enter) pose */
+  HTP_OGE_P_SIDE                                       /* 1 NEAR_SIDE, -1 FAR_SIDE */
+};
+#define HTP_OGE_MAXROWS 32
+#define HTP_OGE_MAXPOLY 32
+#define HTP_OGE_MAXV 12
+enum { HTP_OGE_OK = 0, HTP_OGE_BAD_INPUT = 1, HTP_OGE_NO_ROW_BETWEEN = 2 /* reference: IndexError */,
+       HTP_OGE_OVERFLOW = 3 /* more than MAXPOLY polygons or MAXV vertices */, HTP_OGE_EMPTY_SIDE = 4 };
+typedef struct {
+  int32_t batch, max_rows;  /* max_rows = row stride of the draw arrays */
+  const double* params;     /* [batch][HTP_OGE_NPARAM] */
+  const double* row_draws;  /* [batch][max_rows] */
+  const double* eps_draws;  /* [batch][max_rows] */
+} htp_oge_batch;
+typedef struct {
+  int32_t* status;          /* [batch] HTP_OGE_* */
+  int32_t* n_poly;          /* [batch] */
+  int32_t* n_vert;          /* [batch][MAXPOLY] */
+  double* vertices;         /* [batch][MAXPOLY][MAXV][2] */
+  int32_t* n_facet;         /* [batch][MAXPOLY] facets (-1: fewer than 3 distinct vertices) (nullable) */
+  double* A;                /* [batch][MAXPOLY][MAXV][2] (nullable with n_facet) */
+  double* b;                /* [batch][MAXPOLY][MAXV]    (nullable with n_facet) */
+} htp_oge_result;
+int htp_oge_obstacles_batch(htp_ctx* ctx, const htp_oge_batch* in, htp_oge_result* out);
+int htp_oge_obstacles_batch_device(htp_ctx* ctx, const htp_oge_batch* in, htp_oge_result* out, void* stream);
+double htp_oge_last_ms(htp_ctx* ctx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,7 +23,7 @@ def build():
     subprocess.check_call(["g++", "-O2", "-fno-builtin", "-std=c++17", "-shared", "-fPIC", "-o", SO,
                            os.path.join(CSRC, "htp_hostsim.cpp"), os.path.join(CSRC, "rs_hostsim.cpp"),
                            os.path.join(CSRC, "hastar_hostsim.cpp"), os.path.join(CSRC, "ypark_hostsim.cpp"),
-                           os.path.join(CSRC, "refpath_hostsim.cpp")])
+                           os.path.join(CSRC, "refpath_hostsim.cpp"), os.path.join(CSRC, "oge_hostsim.cpp")])
     return SO
 
 
@@ -138,6 +138,17 @@ def rs_host(queries):
     out["point_offsets"] = np.concatenate([[0], np.cumsum(npts_path)]).astype(np.int64)
     out["n_paths"], out["n_points"] = int(out["path_offsets"][-1]), int(out["point_offsets"][-1])
     return out
+
+
+def oge_host(packed, halfspaces=True):
+    """oge_core.h through the serial host build (same batch/result structs as the GPU).  TEST-ONLY."""
+    L = lib()
+    L.htp_hostsim_oge.argtypes = [ctypes.POINTER(_native.OgeBatch), ctypes.POINTER(_native.OgeResult)]
+    L.htp_hostsim_oge.restype = ctypes.c_int
+    res = _native.OgeResults(packed.batch, halfspaces)
+    b, r = packed.struct(), res.struct()
+    assert L.htp_hostsim_oge(ctypes.byref(b), ctypes.byref(r)) == 0
+    return res
 
 
 def hastar_host(problems, cap_path=4096):

@@ -32,6 +32,9 @@ OUT = os.path.join(ROOT, "tests", "golden", "obca_full")
 
 CASES = ["A:0", "A:1", "A:2", "B:0", "B:1", "B:9", "D:0", "D:33", "D:971", "C:0", "C:1", "C:2", "C:47", "E:0", "E:1",
          "E:12"]
+# Round 3, after configs A-E moved to the reference's scene producers (synth.make_orchard_instance):
+# one converged problem per config plus the host-build screen's failures (profiles/r03h_screen_*.json)
+CASES_R3 = ["A:3", "B:3", "C:3", "D:3", "E:3", "C:36", "C:59", "A:43", "D:347", "D:946"]
 
 
 def run(case):
