@@ -90,7 +90,8 @@ EXPORTS = ["htp_obca_sizes", "htp_create", "htp_destroy", "htp_last_error", "htp
            "htp_init_ref_path_batch", "htp_init_ref_path_batch_device", "htp_init_ref_path_last_ms",
            "htp_queue_create", "htp_queue_destroy", "htp_queue_publish", "htp_queue_close", "htp_queue_published",
            "htp_queue_claimed", "htp_obca_solve_queue_device", "htp_obca_resident_waves",
-           "htp_oge_obstacles_batch", "htp_oge_obstacles_batch_device", "htp_oge_last_ms"]
+           "htp_oge_obstacles_batch", "htp_oge_obstacles_batch_device", "htp_oge_last_ms",
+           "htp_classic_turn_batch", "htp_classic_turn_batch_device", "htp_classic_last_ms"]
 
 
 def _declare(lib):
@@ -174,6 +175,13 @@ def _declare(lib):
     lib.htp_oge_obstacles_batch_device.restype = ctypes.c_int
     lib.htp_oge_last_ms.argtypes = [ctypes.c_void_p]
     lib.htp_oge_last_ms.restype = ctypes.c_double
+    lib.htp_classic_turn_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(CtBatch), ctypes.POINTER(CtResult)]
+    lib.htp_classic_turn_batch.restype = ctypes.c_int
+    lib.htp_classic_turn_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(CtBatch), ctypes.POINTER(CtResult),
+                                                  ctypes.c_void_p]
+    lib.htp_classic_turn_batch_device.restype = ctypes.c_int
+    lib.htp_classic_last_ms.argtypes = [ctypes.c_void_p]
+    lib.htp_classic_last_ms.restype = ctypes.c_double
     return lib
 
 
@@ -711,6 +719,67 @@ class OgeResults:
         return out
 
 
+# ------------------------------------------------------------ classic headland turns (htp_classic.hip)
+CT_NPARAM = 12
+CT_TYPES = {"dubins": 0, "circleback": 1, "fishtail": 2}
+CT_STATUS = {0: "ok", 1: "overflow", 2: "no_word", 3: "bad_input", 4: "rs_error", 5: "no_dubins"}
+
+
+class CtBatch(ctypes.Structure):  # htp_classic_batch
+    _fields_ = [("batch", ctypes.c_int32), ("npoly", ctypes.c_int32), ("nvert", ctypes.c_int32),
+                ("params", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("poly_off", ctypes.c_void_p),
+                ("vertices", ctypes.c_void_p), ("cap_path", ctypes.c_int32), ("cap_samples", ctypes.c_int32)]
+
+
+class CtResult(ctypes.Structure):  # htp_classic_result
+    _fields_ = [("status", ctypes.c_void_p), ("n_path", ctypes.c_void_p), ("path", ctypes.c_void_p)]
+
+
+class ClassicPacked:
+    """Turns for htp_classic_turn_batch.  A turn is a dict: type ("dubins" / "circleback" / "fishtail"), side
+    (map_utils NEAR_SIDE 1 / FAR_SIDE 2), start, end (x, y, yaw), wheel_base, max_steer, radius (the planners'
+    turning-radius argument), step, body (car_poly ring), blockers (obs_poly_list rings; fish-tail only)."""
+
+    def __init__(self, turns, cap_path=4096, cap_samples=4096):
+        B = len(turns)
+        self.batch, self.cap_path, self.cap_samples = B, int(cap_path), int(cap_samples)
+        self.params = np.zeros((B, CT_NPARAM))
+        self.desc = np.zeros((B, 3), np.int32)
+        polys = []
+        for b, t in enumerate(turns):
+            self.params[b] = [CT_TYPES[t["type"]], t.get("side", 1), *np.asarray(t["start"], dtype=np.float64)[:3],
+                              *np.asarray(t["end"], dtype=np.float64)[:3], t["wheel_base"], t["max_steer"],
+                              t["radius"], t.get("step", 0.1)]
+            self.desc[b, 0] = len(polys)
+            polys.append(np.asarray(t["body"], dtype=np.float64).reshape(-1, 2))
+            self.desc[b, 1] = len(polys)
+            polys += [np.asarray(q, dtype=np.float64).reshape(-1, 2) for q in t.get("blockers", [])]
+            self.desc[b, 2] = len(polys)
+        self.poly_off = np.concatenate([[0], np.cumsum([len(q) for q in polys])]).astype(np.int32)
+        self.vertices = np.ascontiguousarray(np.concatenate(polys) if polys else np.zeros((0, 2)))
+
+    def struct(self, ptrs=None):
+        p = ptrs or {}
+        return CtBatch(self.batch, len(self.poly_off) - 1, self.vertices.shape[0],
+                       p.get("params", self.params.ctypes.data), p.get("desc", self.desc.ctypes.data),
+                       p.get("poly_off", self.poly_off.ctypes.data), p.get("vertices", self.vertices.ctypes.data),
+                       self.cap_path, self.cap_samples)
+
+
+class ClassicResults:
+    def __init__(self, packed):
+        B = packed.batch
+        self.status = np.zeros(B, np.int32)
+        self.n_path = np.zeros(B, np.int32)
+        self.path = np.zeros((B, packed.cap_path, 5))
+
+    def struct(self):
+        return CtResult(self.status.ctypes.data, self.n_path.ctypes.data, self.path.ctypes.data)
+
+    def rows(self, b):
+        return self.path[b, :int(self.n_path[b])].copy()
+
+
 class WorkQueue:
     """Host work queue of problem indices feeding one persistent solve launch
     (htp_queue_*: pinned, GPU-coherent host memory)."""
@@ -781,6 +850,17 @@ class Context:
         if rc != 0:
             raise RuntimeError(f"[htp] htp_obca_points_solve_batch failed: {self.error()}")
         return res
+
+    def classic_turns(self, packed):
+        """Batched classic headland turns (host buffers) -> ClassicResults."""
+        r = ClassicResults(packed)
+        b, rs = packed.struct(), r.struct()
+        if self.lib.htp_classic_turn_batch(self.ctx, ctypes.byref(b), ctypes.byref(rs)) != 0:
+            raise RuntimeError(f"[htp] htp_classic_turn_batch failed: {self.error()}")
+        return r
+
+    def classic_last_ms(self):
+        return self.lib.htp_classic_last_ms(self.ctx)
 
     def oge_obstacles(self, packed, halfspaces=True):
         """Batched orchard scene -> OBCA obstacle polygons (+ halfspaces), host buffers -> OgeResults."""

@@ -58,6 +58,9 @@ extern "C" int htp_cpu_obca_solve_range(const htp_obca_batch* in, htp_obca_resul
 
 // Reeds-Shepp words for one pose pair on the host (rs_core.h, the same core as htp_rs_all_paths_batch).
 // Used by the workload generator's fish-tail warm starts (synth.py), which run before any GPU call.
+// The reference's rounding (pure-Python reeds_shepp.py): no a*b+c contraction into FMA, as the device build
+// (rs_core.h's clang pragma); -march=x86-64-v3 would otherwise contract and move a sample's exact-zero pop.
+#pragma GCC optimize("fp-contract=off")
 #include "rs_host.h"
 
 extern "C" int htp_cpu_rs_all_paths(const double* q, int64_t cap_paths, int64_t cap_points, int32_t* n_paths,

@@ -39,6 +39,10 @@ struct htp_ctx {
   hipEvent_t rp_ev0 = nullptr, rp_ev1 = nullptr;
   // orchard scene -> OBCA obstacles (htp_oge.hip)
   hipEvent_t oge_ev0 = nullptr, oge_ev1 = nullptr;
+  // classic turns (htp_classic.hip)
+  void* ct_ws = nullptr;
+  size_t ct_ws_bytes = 0;
+  hipEvent_t ct_ev0 = nullptr, ct_ev1 = nullptr;
 };
 
 static inline int fail(htp_ctx* c, const std::string& m) {

@@ -181,6 +181,8 @@ htp_ctx* htp_create(int32_t device) {
   (void)hipEventCreate(&c->rp_ev1);
   (void)hipEventCreate(&c->oge_ev0);
   (void)hipEventCreate(&c->oge_ev1);
+  (void)hipEventCreate(&c->ct_ev0);
+  (void)hipEventCreate(&c->ct_ev1);
   return c;
 }
 
@@ -206,6 +208,9 @@ void htp_destroy(htp_ctx* c) {
   if (c->rp_ev1) (void)hipEventDestroy(c->rp_ev1);
   if (c->oge_ev0) (void)hipEventDestroy(c->oge_ev0);
   if (c->oge_ev1) (void)hipEventDestroy(c->oge_ev1);
+  if (c->ct_ws) (void)hipFree(c->ct_ws);
+  if (c->ct_ev0) (void)hipEventDestroy(c->ct_ev0);
+  if (c->ct_ev1) (void)hipEventDestroy(c->ct_ev1);
   delete c;
 }
 

@@ -629,7 +629,7 @@ def make_orchard_instance(pid, N=80, M=6, implement="none", key=20251015, turn="
         env = orchard_environment_OBCA(tree_rows, [], tree_width=tree_w, headland_width=6.0)
         try:
             path = _warm_start_path(turn, tree_rows, s_row, e_row, car, empty, env, start, end, exit_off, enter_off)
-        except (ValueError, IndexError, ZeroDivisionError):
+        except (ValueError, IndexError, ZeroDivisionError, RuntimeError):
             path = None
         if path is None or len(path) < 4:
             continue
@@ -652,10 +652,13 @@ def make_orchard_instance(pid, N=80, M=6, implement="none", key=20251015, turn="
         pts = np.concatenate([f.reshape(-1, 2) for f in foot])
         hw = max(6.0, _needed_headland(tree_rows, pts, env.get_headland_angle(env.NEAR_SIDE)) + margin)
         env = orchard_environment_OBCA(tree_rows, [], tree_width=tree_w, headland_width=hw)
-        with _legacy_random(seed + 1):
-            boundary = env.create_boundary_polygons()
-        row_polys = env.get_obstacle_tree_rows(start, end)
-        obs = env.get_obstacles_for_OBCA(boundary, row_polys, start, end, side=env.NEAR_SIDE)
+        try:   # the reference raises IndexError when no boundary piece lies beside the turn: redraw
+            with _legacy_random(seed + 1):
+                boundary = env.create_boundary_polygons()
+            row_polys = env.get_obstacle_tree_rows(start, end)
+            obs = env.get_obstacles_for_OBCA(boundary, row_polys, start, end, side=env.NEAR_SIDE)
+        except (IndexError, ValueError):
+            continue
         pool = [q for o in obs for q in _split_quads(o)]
         if len(pool) < M:   # the rest of the orchard: other tree rows (nearest first), the other bound quad
             used_rows = {round(float(np.mean(np.asarray(p)[:, 1])), 6) for p in row_polys}
@@ -689,7 +692,8 @@ def make_orchard_instance(pid, N=80, M=6, implement="none", key=20251015, turn="
         x_bound=[-np.inf, np.inf], y_bound=[-np.inf, np.inf],
         meta=dict(pid=pid, turn=turn, length=Lp, start=tuple(start), goal=tuple(end), s_row=s_row, e_row=e_row,
                   headland_width=hw, n_producer=len(obs), n_dummy=k, l_std=l_std, nrows=rows_n, row_width=row_w,
-                  row_length=row_len, slope=slope, tree_width=tree_w, seed=seed),
+                  row_length=row_len, slope=slope, tree_width=tree_w, seed=seed, exit_off=exit_off,
+                  enter_off=enter_off),
     )
     for kk, vv in over.items():
         inst[kk] = vv
@@ -724,6 +728,44 @@ def orchard_obstacles_host(meta):
         boundary = env.create_boundary_polygons()
     row_polys = env.get_obstacle_tree_rows(meta["start"], meta["goal"])
     return env.get_obstacles_for_OBCA(boundary, row_polys, meta["start"], meta["goal"], side=env.NEAR_SIDE)
+
+
+def _orchard_env(meta):
+    from .path_planner import map_utils
+    from .path_planner.OGE_OBCA import orchard_environment_OBCA
+    with _legacy_random(meta["seed"]):
+        rows = map_utils.create_tree_rows(int(meta["nrows"]), meta["row_width"], meta["row_length"],
+                                          slope_angle=meta["slope"], l_std=meta["l_std"])
+    return rows, orchard_environment_OBCA(rows, [], tree_width=meta["tree_width"], headland_width=6.0)
+
+
+def classic_turn(meta):
+    """The warm-start planner call of a make_orchard_instance problem as the device planner takes it
+    (htp_classic_turn_batch, _native.ClassicPacked): turn type, row poses, car, and the blocker polygons
+    (env.obs_poly_list) the fish-tail's footprint checks use."""
+    from .path_planner.geom import ring_of
+    _, env = _orchard_env(meta)
+    veh = VEHICLE
+    body = geometry.body_rectangle(veh["axle_to_front"], veh["axle_to_back"], veh["width"])
+    r = 1.0 / (math.tan(veh["max_steer"]) / veh["wheelbase"])
+    return dict(type=meta["turn"], side=1, start=meta["start"], end=meta["goal"], wheel_base=veh["wheelbase"],
+                max_steer=veh["max_steer"], radius=r, step=0.1, body=body,
+                blockers=[ring_of(q) for q in env.obs_poly_list])
+
+
+def classic_turn_host(meta, implement="none"):
+    """The same call through the host planners (path_planner/, the restated reference) -> rows [x, y, yaw, k, dir]."""
+    from .path_planner.car_model import CarModel
+    rows, env = _orchard_env(meta)
+    veh = VEHICLE
+    feat = IMPLEMENTS[implement]
+    car = CarModel(max_steer=veh["max_steer"], wheel_base=veh["wheelbase"], axle_to_front=veh["axle_to_front"],
+                   axle_to_back=veh["axle_to_back"], width=veh["width"],
+                   aux_poly_features=[feat] if feat is not None else [], with_aux=feat is not None)
+    empty = CarModel(max_steer=veh["max_steer"], wheel_base=veh["wheelbase"], axle_to_front=veh["axle_to_front"],
+                     axle_to_back=veh["axle_to_back"], width=veh["width"], with_aux=False)
+    return _warm_start_path(meta["turn"], rows, meta["s_row"], meta["e_row"], car, empty, env,
+                            np.asarray(meta["start"]), np.asarray(meta["goal"]), meta["exit_off"], meta["enter_off"])
 
 
 # turn types of the BASELINE configs: A fish-tail, B Omega/circle-back, C mixed, D/E the Dubins turn

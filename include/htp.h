@@ -404,6 +404,40 @@ int htp_oge_obstacles_batch(htp_ctx* ctx, const htp_oge_batch* in, htp_oge_resul
 int htp_oge_obstacles_batch_device(htp_ctx* ctx, const htp_oge_batch* in, htp_oge_result* out, void* stream);
 double htp_oge_last_ms(htp_ctx* ctx);
 
+/* ---------------------------------------------------------------------------
+ * Classic headland turns: one warm-start path per problem,
+ * rows [x, y, yaw, k, dir] as the reference's planners return them (csrc/classic_core.h):
+ *   HTP_CT_DUBINS      get_dubins_path_full(start, end, R, step)   safety_forward_path_plan.py:286-297
+ *   HTP_CT_CIRCLEBACK  get_circle_back_path_full(start, end, R, car, side, step)   :395-454
+ *   HTP_CT_FISHTAIL    get_start_end_pose_for_reeds_shepp (:300-364) + the collision-free Reeds-Shepp word
+ *                      with the least backward length + Dubins lead-in/out (R/test/classic_planner.ipynb 10-11)
+ * Footprints (fish-tail only): the body polygon at every pose against the blocker polygons
+ * (check_path_feasibility :423-458, boundary_check=False); polygons in CSR pools as for the searches. */
+#define HTP_CT_NPARAM 12
+enum { HTP_CT_P_TYPE = 0, HTP_CT_P_SIDE,                      /* HTP_CT_* ; map_utils NEAR_SIDE 1 / FAR_SIDE 2 */
+       HTP_CT_P_SX, HTP_CT_P_SY, HTP_CT_P_SYAW, HTP_CT_P_EX, HTP_CT_P_EY, HTP_CT_P_EYAW,
+       HTP_CT_P_WB, HTP_CT_P_MAXSTEER, HTP_CT_P_RADIUS, HTP_CT_P_STEP };
+enum { HTP_CT_DUBINS = 0, HTP_CT_CIRCLEBACK = 1, HTP_CT_FISHTAIL = 2 };
+enum { HTP_CT_OK = 0, HTP_CT_OVERFLOW = 1, HTP_CT_NO_WORD = 2 /* no collision-free word (reference: None) */,
+       HTP_CT_BAD_INPUT = 3, HTP_CT_RS_ERROR = 4 /* reference raises in reeds_shepp */, HTP_CT_NO_DUBINS = 5 };
+typedef struct {
+  int32_t batch, npoly, nvert;
+  const double* params;     /* [batch][HTP_CT_NPARAM] */
+  const int32_t* desc;      /* [batch][3]: body polygon id, blockers [blk0, blk1) */
+  const int32_t* poly_off;  /* [npoly+1] */
+  const double* vertices;   /* [nvert][2] */
+  int32_t cap_path;         /* rows per problem in `path` */
+  int32_t cap_samples;      /* Dubins samples per piece (scratch sizing) */
+} htp_classic_batch;
+typedef struct {
+  int32_t* status;          /* [batch] HTP_CT_* */
+  int32_t* n_path;          /* [batch] */
+  double* path;             /* [batch][cap_path][5] x, y, yaw, k, dir */
+} htp_classic_result;
+int htp_classic_turn_batch(htp_ctx* ctx, const htp_classic_batch* in, htp_classic_result* out);
+int htp_classic_turn_batch_device(htp_ctx* ctx, const htp_classic_batch* in, htp_classic_result* out, void* stream);
+double htp_classic_last_ms(htp_ctx* ctx);
+
 #ifdef __cplusplus
 }
 #endif

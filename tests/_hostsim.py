@@ -23,7 +23,8 @@ def build():
     subprocess.check_call(["g++", "-O2", "-fno-builtin", "-std=c++17", "-shared", "-fPIC", "-o", SO,
                            os.path.join(CSRC, "htp_hostsim.cpp"), os.path.join(CSRC, "rs_hostsim.cpp"),
                            os.path.join(CSRC, "hastar_hostsim.cpp"), os.path.join(CSRC, "ypark_hostsim.cpp"),
-                           os.path.join(CSRC, "refpath_hostsim.cpp"), os.path.join(CSRC, "oge_hostsim.cpp")])
+                           os.path.join(CSRC, "refpath_hostsim.cpp"), os.path.join(CSRC, "oge_hostsim.cpp"),
+                           os.path.join(CSRC, "classic_hostsim.cpp")])
     return SO
 
 
@@ -148,6 +149,17 @@ def oge_host(packed, halfspaces=True):
     res = _native.OgeResults(packed.batch, halfspaces)
     b, r = packed.struct(), res.struct()
     assert L.htp_hostsim_oge(ctypes.byref(b), ctypes.byref(r)) == 0
+    return res
+
+
+def classic_host(packed):
+    """classic_core.h through the serial host build (same batch/result structs as the GPU).  TEST-ONLY."""
+    L = lib()
+    L.htp_hostsim_classic.argtypes = [ctypes.POINTER(_native.CtBatch), ctypes.POINTER(_native.CtResult)]
+    L.htp_hostsim_classic.restype = ctypes.c_int
+    res = _native.ClassicResults(packed)
+    b, r = packed.struct(), res.struct()
+    assert L.htp_hostsim_classic(ctypes.byref(b), ctypes.byref(r)) == 0
     return res
 
 

@@ -70,6 +70,16 @@ FAILURE_CLASS_ONLY = {
     # Infeasible_Problem_Detected (7) (host: 2189 iterations / 45 phases)
     "E6": "3 vs 7",
 }
+# Fixtures the oracle does not solve but the device does: the iterates separate at rounding level inside a
+# long restoration cycle (the host build of the same source follows the oracle) and the device run leaves
+# the cycle at a KKT point of the reference's NLP.  The device must then either end with the oracle's
+# status or return a point that passes the KKT checks below (primal feasibility <= 1e-4 and the
+# least-squares stationarity residual <= 1e-5): a solution of the same NLP.
+DIVERGENT_AFTER_RESTORATION = {
+    # oracle: Infeasible_Problem_Detected after 516 iterations / 41 restoration phases (host build: 7 after
+    # 511); device: Solve_Succeeded after 708
+    "D347": "7 vs 0",
+}
 
 
 def _golden():
@@ -94,6 +104,11 @@ def test_full_config_parity_vs_oracle_fixtures(ctx, cfg, pid, path):
     if f"{cfg}{pid}" in FAILURE_CLASS_ONLY:
         # both fail; which failure status ends a long restoration cycle is decided by rounding
         assert st not in (0, 1) and res.status[0] not in (0, 1), (res.status[0], st)
+        return
+    if f"{cfg}{pid}" in DIVERGENT_AFTER_RESTORATION and res.status[0] in (0, 1) and st not in (0, 1):
+        nlp = ObcaNLP(inst)
+        cv, bv = _kkt_residuals(nlp, res.x[0])
+        assert cv <= 1e-4 and bv <= 1e-12 and _stationarity(nlp, res.x[0]) <= 1e-5, (cv, bv)
         return
     assert res.status[0] == st, (res.status[0], st, int(res.iterations[0]), int(g["iters"]))
     # the restoration phases the oracle needed are taken on the device too

@@ -1,5 +1,6 @@
 #!/bin/bash
-# round-3 GPU step h: the reference-producer workload (tests, smoke, default bench) and a compiler-flag A/B
+# round-3 GPU step h: the reference-producer workload (all GPU tests, smoke, default bench) and a
+# compiler-flag A/B.  Test failures do not stop the run (a fault / timeout does).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -8,5 +9,11 @@ T=${1:-r03h}
 ( while true; do date >> gpurun_out/heartbeat.log; sleep 20; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-bash tools/gpu_evidence.sh $T tests bench || exit $?
-timeout -k 10 400 python -u tools/ab_phase.py D 4096 base trk pav o2 > gpurun_out/${T}_ab.txt 2>&1 || exit $?
+timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/${T}_gputest.out 2>&1
+rc=$?; echo "gputest rc=$rc"; tail -3 gpurun_out/${T}_gputest.out
+case $rc in 0|1) ;; *) exit $rc ;; esac
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.out 2>&1 || exit $?
+tail -1 gpurun_out/${T}_smoke.out
+timeout -k 10 400 python -u bench.py > gpurun_out/${T}_bench.out 2> gpurun_out/${T}_bench.err || exit $?
+tail -1 gpurun_out/${T}_bench.out | cut -c1-400
+timeout -k 10 400 python -u tools/ab_phase.py D 4096 base trk pav o2 outl unr1 > gpurun_out/${T}_ab.txt 2>&1 || exit $?
