@@ -91,7 +91,8 @@ EXPORTS = ["htp_obca_sizes", "htp_create", "htp_destroy", "htp_last_error", "htp
            "htp_queue_create", "htp_queue_destroy", "htp_queue_publish", "htp_queue_close", "htp_queue_published",
            "htp_queue_claimed", "htp_obca_solve_queue_device", "htp_obca_resident_waves",
            "htp_oge_obstacles_batch", "htp_oge_obstacles_batch_device", "htp_oge_last_ms",
-           "htp_classic_turn_batch", "htp_classic_turn_batch_device", "htp_classic_last_ms"]
+           "htp_classic_turn_batch", "htp_classic_turn_batch_device", "htp_classic_last_ms",
+           "htp_orchard_chain_device", "htp_chain_last_ms"]
 
 
 def _declare(lib):
@@ -182,6 +183,10 @@ def _declare(lib):
     lib.htp_classic_turn_batch_device.restype = ctypes.c_int
     lib.htp_classic_last_ms.argtypes = [ctypes.c_void_p]
     lib.htp_classic_last_ms.restype = ctypes.c_double
+    lib.htp_orchard_chain_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChainBatch), ctypes.c_void_p]
+    lib.htp_orchard_chain_device.restype = ctypes.c_int
+    lib.htp_chain_last_ms.argtypes = [ctypes.c_void_p]
+    lib.htp_chain_last_ms.restype = ctypes.c_double
     return lib
 
 
@@ -780,6 +785,15 @@ class ClassicResults:
         return self.path[b, :int(self.n_path[b])].copy()
 
 
+class ChainBatch(ctypes.Structure):  # htp_chain_batch
+    _fields_ = [("batch", ctypes.c_int32), ("N", ctypes.c_int32), ("M", ctypes.c_int32),
+                ("scenes", OgeBatch), ("turns", CtBatch), ("margin", ctypes.c_void_p),
+                ("n_vpoly", ctypes.c_int32), ("vpoly_nv", ctypes.c_int32 * 2), ("vpoly", ctypes.c_double * 32),
+                ("dT", ctypes.c_double), ("wheel_base", ctypes.c_double), ("cap_rows", ctypes.c_int32),
+                ("traj", ctypes.c_void_p), ("obs_A", ctypes.c_void_p), ("obs_b", ctypes.c_void_p),
+                ("status", ctypes.c_void_p)]
+
+
 class WorkQueue:
     """Host work queue of problem indices feeding one persistent solve launch
     (htp_queue_*: pinned, GPU-coherent host memory)."""
@@ -821,6 +835,7 @@ class Context:
 
     def __init__(self, device=0, options=None, lib=None):
         self.lib = lib or load()
+        self.device = int(device)
         self.ctx = self.lib.htp_create(int(device))
         if not self.ctx:
             raise RuntimeError("[htp] htp_create failed")

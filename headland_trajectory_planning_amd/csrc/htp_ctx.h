@@ -43,6 +43,10 @@ struct htp_ctx {
   void* ct_ws = nullptr;
   size_t ct_ws_bytes = 0;
   hipEvent_t ct_ev0 = nullptr, ct_ev1 = nullptr;
+  // orchard workload chain (htp_chain.hip)
+  void* ch_ws = nullptr;
+  size_t ch_ws_bytes = 0;
+  hipEvent_t ch_ev0 = nullptr, ch_ev1 = nullptr;
 };
 
 static inline int fail(htp_ctx* c, const std::string& m) {

@@ -183,6 +183,8 @@ htp_ctx* htp_create(int32_t device) {
   (void)hipEventCreate(&c->oge_ev1);
   (void)hipEventCreate(&c->ct_ev0);
   (void)hipEventCreate(&c->ct_ev1);
+  (void)hipEventCreate(&c->ch_ev0);
+  (void)hipEventCreate(&c->ch_ev1);
   return c;
 }
 
@@ -211,6 +213,9 @@ void htp_destroy(htp_ctx* c) {
   if (c->ct_ws) (void)hipFree(c->ct_ws);
   if (c->ct_ev0) (void)hipEventDestroy(c->ct_ev0);
   if (c->ct_ev1) (void)hipEventDestroy(c->ct_ev1);
+  if (c->ch_ws) (void)hipFree(c->ch_ws);
+  if (c->ch_ev0) (void)hipEventDestroy(c->ch_ev0);
+  if (c->ch_ev1) (void)hipEventDestroy(c->ch_ev1);
   delete c;
 }
 

@@ -693,7 +693,7 @@ def make_orchard_instance(pid, N=80, M=6, implement="none", key=20251015, turn="
         meta=dict(pid=pid, turn=turn, length=Lp, start=tuple(start), goal=tuple(end), s_row=s_row, e_row=e_row,
                   headland_width=hw, n_producer=len(obs), n_dummy=k, l_std=l_std, nrows=rows_n, row_width=row_w,
                   row_length=row_len, slope=slope, tree_width=tree_w, seed=seed, exit_off=exit_off,
-                  enter_off=enter_off),
+                  enter_off=enter_off, margin=margin, implement=implement),
     )
     for kk, vv in over.items():
         inst[kk] = vv

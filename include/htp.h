@@ -438,6 +438,33 @@ int htp_classic_turn_batch(htp_ctx* ctx, const htp_classic_batch* in, htp_classi
 int htp_classic_turn_batch_device(htp_ctx* ctx, const htp_classic_batch* in, htp_classic_result* out, void* stream);
 double htp_classic_last_ms(htp_ctx* ctx);
 
+/* ---------------------------------------------------------------------------
+ * Orchard workload chain on the device (synth.make_orchard_instance's steps after the scene draws): for each
+ * problem, the classic turn (htp_classic_turn_batch) -> get_init_ref_path at ds = L / (N - 1) / 2,
+ * desired_v = min(ds / dT, 0.9) (R/obca_py/util.py:62-113) -> the init guess resampled to N rows and the
+ * headland width the warm start needs -> the OGE_OBCA obstacle producer (htp_oge_obstacles_batch) -> quads,
+ * the M nearest, halfspaces.  Writes the htp_obca_batch arrays traj / obs_A / obs_b (4 edges per obstacle)
+ * in HBM, enqueued on `stream`; intermediates live in the context.  `scenes` and `turns` hold device
+ * pointers; scenes.params[b][HTP_OGE_P_HW] is overwritten with the chain's headland width. */
+typedef struct {
+  int32_t batch, N, M;
+  htp_oge_batch scenes;            /* device */
+  htp_classic_batch turns;         /* device pools */
+  const double* margin;            /* [batch] device: boundary margin behind the warm start */
+  int32_t n_vpoly;                 /* vehicle footprint polygons (car frame): body, then the implement (<= 2) */
+  int32_t vpoly_nv[2];
+  double vpoly[2][8][2];
+  double dT, wheel_base;
+  int32_t cap_rows;                /* init-guess rows per problem */
+  double* traj;                    /* [batch][N][5] device out */
+  double* obs_A;                   /* [batch][4 M][2] device out */
+  double* obs_b;                   /* [batch][4 M] device out */
+  int32_t* status;                 /* [batch] device out: 0, or 16 * stage + that stage's status
+                                      (stage 1 classic, 2 init guess, 3 obstacle producer, 4 quads) */
+} htp_chain_batch;
+int htp_orchard_chain_device(htp_ctx* ctx, const htp_chain_batch* in, void* stream);
+double htp_chain_last_ms(htp_ctx* ctx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,4 +16,6 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -1 gpurun_out/${T}_smoke.out
 timeout -k 10 400 python -u bench.py > gpurun_out/${T}_bench.out 2> gpurun_out/${T}_bench.err || exit $?
 tail -1 gpurun_out/${T}_bench.out | cut -c1-400
-timeout -k 10 400 python -u tools/ab_phase.py D 4096 base trk pav o2 outl unr1 > gpurun_out/${T}_ab.txt 2>&1 || exit $?
+timeout -k 10 400 python -u tools/ab_phase.py D 4096 base trk pav o2 outl unr1 os > gpurun_out/${T}_ab.txt 2>&1 || exit $?
+timeout -k 10 400 python -u bench.py --e2e --config C --batch 4096 --steps 2 --warmup 1 > gpurun_out/${T}_e2eC.out 2> gpurun_out/${T}_e2eC.err || exit $?
+tail -1 gpurun_out/${T}_e2eC.out | cut -c1-400
