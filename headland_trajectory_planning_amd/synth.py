@@ -637,6 +637,13 @@ def make_orchard_instance(pid, N=80, M=6, implement="none", key=20251015, turn="
         # orchard_geometry_environment.py:423-458): a planner output that fails it is redrawn
         if not env.check_path_feasibility(car, path[:, :3], boundary_check=False, aux_check=True):
             continue
+        # a forward Dubins turn is the reference's first choice only when it clears the rows buffered to
+        # tree_width_in_forward_plan (headland_planner_y_type_park_combined, headland_path_planning.py:55-121;
+        # 0.4 in R/test/obca.ipynb) -- otherwise the reference plans a Y-park + hybrid A* turn instead
+        if turn == "dubins":
+            env_fwd = orchard_environment_OBCA(tree_rows, [], tree_width=0.4, headland_width=6.0)
+            if not env_fwd.check_path_feasibility(empty, path[:, :3], boundary_check=False):
+                continue
         Lp = float(np.sum(np.hypot(np.diff(path[:, 0]), np.diff(path[:, 1]))))
         ds = Lp / (N - 1)
         desired_v = min(ds / dT, 0.9)
