@@ -572,6 +572,16 @@ def _needed_headland(tree_rows, pts, angle):
     return float(np.max(xr - pts[:, 0])) * abs(math.sin(angle))
 
 
+def _tree_row_range(tree_rows, start, end):
+    """Row indices [a, c) get_obstacle_tree_rows (OGE_OBCA.py:477-591) turns into obstacles."""
+    hi, lo = max(start[1], end[1]), min(start[1], end[1])
+    idxs = np.sort(np.where((tree_rows[:, 0, 1] > lo) & (tree_rows[:, 0, 1] < hi))[0])
+    n = len(tree_rows)
+    if idxs[0] == idxs[-1]:
+        return max(idxs[-1] - 2, 0), min(idxs[-1] + 2, n - 1)
+    return max(idxs[0] - 2, 0), min(idxs[-1] + 3, n - 1)
+
+
 def make_orchard_instance(pid, N=80, M=6, implement="none", key=20251015, turn="dubins", **over):
     """One OBCA instance whose scene and warm start come from the reference's producers (see the block
     comment above).  Draws per attempt: row width U[2.2, 3.5], slope U[-15, 15] deg, l_std in {0, 1},
@@ -668,10 +678,9 @@ def make_orchard_instance(pid, N=80, M=6, implement="none", key=20251015, turn="
             continue
         pool = [q for o in obs for q in _split_quads(o)]
         if len(pool) < M:   # the rest of the orchard: other tree rows (nearest first), the other bound quad
-            used_rows = {round(float(np.mean(np.asarray(p)[:, 1])), 6) for p in row_polys}
+            a, c = _tree_row_range(tree_rows, start, end)
             mid = 0.5 * (start[1] + end[1])
-            extra = sorted((abs(r[0, 1] - mid), i) for i, r in enumerate(tree_rows)
-                           if round(float(r[0, 1]), 6) not in used_rows)
+            extra = sorted((abs(r[0, 1] - mid), i) for i, r in enumerate(tree_rows) if not a <= i < c)
             pool += [env._row_rect(tree_rows[i], False) for _, i in extra]
             pool += [p for p in (boundary[3] if start[1] > end[1] else boundary[2])]
         gaps = np.array([min(_min_sat_gap(f, q) for f in foot) for q in pool])

@@ -24,7 +24,7 @@ def build():
                            os.path.join(CSRC, "htp_hostsim.cpp"), os.path.join(CSRC, "rs_hostsim.cpp"),
                            os.path.join(CSRC, "hastar_hostsim.cpp"), os.path.join(CSRC, "ypark_hostsim.cpp"),
                            os.path.join(CSRC, "refpath_hostsim.cpp"), os.path.join(CSRC, "oge_hostsim.cpp"),
-                           os.path.join(CSRC, "classic_hostsim.cpp")])
+                           os.path.join(CSRC, "classic_hostsim.cpp"), os.path.join(CSRC, "chain_hostsim.cpp")])
     return SO
 
 
@@ -150,6 +150,39 @@ def oge_host(packed, halfspaces=True):
     b, r = packed.struct(), res.struct()
     assert L.htp_hostsim_oge(ctypes.byref(b), ctypes.byref(r)) == 0
     return res
+
+
+def chain_host(inputs):
+    """The orchard workload chain (chain_core.h) through the serial host build -> (instances, status).
+    `inputs` from e2e.host_inputs.  TEST-ONLY."""
+    L = lib()
+    L.htp_hostsim_chain.argtypes = [ctypes.POINTER(_native.ChainBatch)]
+    L.htp_hostsim_chain.restype = ctypes.c_int
+    sc, tu = inputs["scenes"], inputs["turns"]
+    B, N, M = sc.batch, inputs["N"], inputs["M"]
+    params = sc.params.copy()
+    traj, A, b = np.zeros((B, N, 5)), np.zeros((B, 4 * M, 2)), np.zeros((B, 4 * M))
+    status = np.zeros(B, np.int32)
+    cb = _native.ChainBatch()
+    cb.batch, cb.N, cb.M = B, N, M
+    cb.scenes = sc.struct({"params": params.ctypes.data})
+    cb.turns = tu.struct()
+    margin = np.ascontiguousarray(inputs["margin"], dtype=np.float64)
+    cb.margin = margin.ctypes.data
+    cb.n_vpoly = len(inputs["polys"])
+    vp = np.zeros((2, 8, 2))
+    for k, p in enumerate(inputs["polys"]):
+        cb.vpoly_nv[k] = p.shape[0]
+        vp[k, :p.shape[0]] = p
+    for i, v in enumerate(vp.reshape(-1)):
+        cb.vpoly[i] = float(v)
+    t = inputs["template"]
+    cb.dT, cb.wheel_base, cb.cap_rows = float(t["dT"]), 1.9, 1024
+    cb.traj, cb.obs_A, cb.obs_b, cb.status = traj.ctypes.data, A.ctypes.data, b.ctypes.data, status.ctypes.data
+    assert L.htp_hostsim_chain(ctypes.byref(cb)) == 0
+    insts = [dict(init_traj=traj[k], obs_A=[A[k, 4 * m:4 * m + 4] for m in range(M)],
+                  obs_b=[b[k, 4 * m:4 * m + 4] for m in range(M)]) for k in range(B)]
+    return insts, status
 
 
 def classic_host(packed):
