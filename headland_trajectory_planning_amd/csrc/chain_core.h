@@ -5,7 +5,7 @@
 //
 //   prep ..... the turn's length (np.sum of np.hypot of the path steps: numpy's pairwise summation),
 //              ds = L / (N - 1), desired_v = min(ds / dT, 0.9): get_init_ref_path's inputs
-//              (R/obca_py/util.py:62-113 at ds / 2)
+//              (R/obca_py/util.py:62-113 at spacing L / (2 N - 1.5))
 //   resample . the init guess at N rows of even arc length (synth._resample_rows) and the headland width
 //              the warm start needs (synth._needed_headland over the footprint of both pose sets):
 //              max(6, needed + margin) -> the orchard producer's headland_width
@@ -141,7 +141,7 @@ HTP_HD inline void prep(const double* rows, int n, int N, double dT, double wb, 
   const double dv = ds / dT;
   rp_params[0] = wb;
   rp_params[1] = dv < 0.9 ? dv : 0.9;   // min(ds / dT, 0.9)
-  rp_params[2] = ds / 2.0;
+  rp_params[2] = Lp / (2.0 * N - 1.5);   // synth: off the integer sample-count boundary of a one-gear turn
 }
 
 // ---- resample (synth._resample_rows) + the headland width the warm start needs (lane 0)

@@ -28,14 +28,15 @@ def host_inputs(metas, cfg):
 class DeviceChain:
     """Device buffers (torch) for one batch of the chain and the OBCA solve of its output."""
 
-    def __init__(self, ctx, inputs, cap_rows=1024):
+    def __init__(self, ctx, inputs, cap_rows=1024, copies=1):
         import torch
         self.ctx, self.torch = ctx, torch
         dev = torch.device("cuda", ctx.device)
         self.dev = dev
         sc, tu = inputs["scenes"], inputs["turns"]
         B, N, M = sc.batch, inputs["N"], inputs["M"]
-        self.B, self.N, self.M, self.cap_rows = B, N, M, cap_rows
+        self.B, self.N, self.M, self.cap_rows, self.copies = B, N, M, cap_rows, copies
+        B = B * copies   # output slots: one slice of B problems per build(k)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
         self.sc_in = {k: t(getattr(sc, k)) for k in ("params", "row_draws", "eps_draws")}
         self.tu_in = {k: t(getattr(tu, k)) for k in ("params", "desc", "poly_off", "vertices")}
@@ -53,7 +54,7 @@ class DeviceChain:
         self.obs_edges = np.full(M, 4, np.int32)
         self.time_opt = int(np.asarray(tmpl["W"])[1, 1] != 0)
         cb = _native.ChainBatch()
-        cb.batch, cb.N, cb.M = B, N, M
+        cb.batch, cb.N, cb.M = self.B, N, M
         cb.scenes = sc.struct({k: v.data_ptr() for k, v in self.sc_in.items()})
         cb.turns = tu.struct({k: v.data_ptr() for k, v in self.tu_in.items()})
         cb.margin = self.margin.data_ptr()
@@ -71,12 +72,22 @@ class DeviceChain:
         cb.status = self.status.data_ptr()
         self.cb = cb
 
-    def build(self, stream=None):
-        """Enqueue the chain on `stream` (a torch.cuda.Stream; default: the current stream)."""
+    def build(self, stream=None, copy=0):
+        """Enqueue the chain on `stream` (a torch.cuda.Stream; default: the current stream), writing output
+        slice `copy` (problems [copy * B, (copy + 1) * B))."""
         s = stream or self.torch.cuda.current_stream(self.dev)
-        if self.ctx.lib.htp_orchard_chain_device(self.ctx.ctx, ctypes.byref(self.cb),
-                                                 ctypes.c_void_p(s.cuda_stream)) != 0:
+        cb = self.cb
+        o = copy * self.B
+        cb.traj = self.traj[o:].data_ptr()
+        cb.obs_A, cb.obs_b, cb.status = self.obs_A[o:].data_ptr(), self.obs_b[o:].data_ptr(), self.status[o:].data_ptr()
+        if self.ctx.lib.htp_orchard_chain_device(self.ctx.ctx, ctypes.byref(cb), ctypes.c_void_p(s.cuda_stream)) != 0:
             raise RuntimeError(f"[htp] htp_orchard_chain_device failed: {self.ctx.error()}")
+
+    def struct(self, ptrs=None):
+        """PackedBatch-style hook: htp_obca_batch over every output slot (for the persistent launch)."""
+        b = self.obca_batch()
+        b.batch = self.B * self.copies
+        return b
 
     def obca_batch(self):
         """htp_obca_batch over the chain's device outputs (+ the constant body / parameter arrays)."""
@@ -92,7 +103,7 @@ class DeviceChain:
         """The device-built problems as host instance dicts (oracle/nlp.py format), for checks."""
         traj, A, bb = self.traj.cpu().numpy(), self.obs_A.cpu().numpy(), self.obs_b.cpu().numpy()
         out = []
-        for k in range(self.B):
+        for k in range(self.B * self.copies):
             out.append(dict(init_traj=traj[k], obs_A=[A[k, 4 * m:4 * m + 4] for m in range(self.M)],
                             obs_b=[bb[k, 4 * m:4 * m + 4] for m in range(self.M)]))
         return out
@@ -119,8 +130,9 @@ def solve_chain(ctx, chain, outs, stream):
 
 
 def run_bench(insts, cfg, steps, warmup, max_cpu_time=20.0, device=0):
-    """Time `steps` passes of chain + solve over the problems whose make_orchard_instance metas `insts`
-    carry; returns the bench line fields."""
+    """Time `steps` passes of chain + solve over the problems whose make_orchard_instance metas `insts` carry:
+    the chain runs once per step (into its own output slice), then one persistent OBCA launch fed by a work
+    queue solves every step's problems (as bench.py's headline job), all on one stream."""
     import time
 
     import torch
@@ -128,40 +140,43 @@ def run_bench(insts, cfg, steps, warmup, max_cpu_time=20.0, device=0):
     inputs = host_inputs(metas, cfg)
     ctx = _native.Context(device)
     ctx.set_option("max_cpu_time", max_cpu_time)
-    chain = DeviceChain(ctx, inputs)
+    chain = DeviceChain(ctx, inputs, copies=max(steps, warmup, 1))
     dev = chain.dev
     n_var = _native.PackedBatch([inputs["template"]]).n_var
-    outs = solve_outputs(torch, dev, chain.B, n_var)
+    outs = solve_outputs(torch, dev, chain.B * chain.copies, n_var)
+    optr = {k: v.data_ptr() for k, v in outs.items()}
+    waves = ctx.resident_waves(chain)
     stream = torch.cuda.Stream(dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    chain_ms, solve_ms = [], []
 
-    def step():
+    def job(k):
+        T = k * chain.B
+        q = _native.WorkQueue(ctx, T)
         ev[0].record(stream)
-        chain.build(stream)
+        for c in range(k):
+            chain.build(stream, copy=c)
         ev[1].record(stream)
-        solve_chain(ctx, chain, outs, stream)
-        ev[2].record(stream)
+        try:
+            ctx.solve_queue_device(chain, None, q, optr, stream=stream.cuda_stream, waves=waves)
+            ev[2].record(stream)
+            q.publish(np.arange(T, dtype=np.int32))
+        finally:
+            q.close()
         stream.synchronize()
-        chain_ms.append(ev[0].elapsed_time(ev[1]))
-        solve_ms.append(ev[1].elapsed_time(ev[2]))
+        return ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), T
 
-    for _ in range(warmup):
-        step()
-    chain_ms.clear()
-    solve_ms.clear()
+    if warmup:
+        job(warmup)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    chain_ms, solve_ms, T = job(steps)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    st = outs["status"].cpu().numpy()
-    it = outs["iterations"].cpu().numpy()
-    chain_st = chain.status.cpu().numpy()
-    return dict(value=chain.B * steps / elapsed, elapsed=elapsed, chain_ms=float(np.mean(chain_ms)),
-                solve_ms=float(np.mean(solve_ms)), chain_status={str(k): int(v) for k, v in
-                                                                  zip(*np.unique(chain_st, return_counts=True))},
+    st = outs["status"][:T].cpu().numpy()
+    it = outs["iterations"][:T].cpu().numpy()
+    chain_st = chain.status[:T].cpu().numpy()
+    return dict(value=T / elapsed, elapsed=elapsed, chain_ms=chain_ms / steps, solve_ms=solve_ms / steps,
+                chain_status={str(k): int(v) for k, v in zip(*np.unique(chain_st, return_counts=True))},
                 status_counts={str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
                 success_rate=float(np.isin(st, [0, 1]).mean()), mean_iters=float(it.mean()), batch=chain.B,
-                iters_sum=float(it.sum()))
+                iters_sum=float(it.sum()), waves=waves)
