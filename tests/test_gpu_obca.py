@@ -157,7 +157,7 @@ def test_full_config_properties(ctx, cfg, nprob, min_ok):
     """Configs at their turn types and scenes (synth.config_instance: the reference's producers)."""
     insts = [synth.config_instance(cfg, pid) for pid in range(nprob)]
     pk = _native.PackedBatch(insts)
-    # config E (N=160, 12 obstacles, pruner) is restoration-heavy (E3: 712 iterations / 29 restoration phases
+    # config E (N=160, 12 obstacles, pruner) is restoration-heavy (E3: 356 iterations / 30 restoration phases
     # in the oracle too); it runs under the reference's default max_cpu_time (optimizer.py:475)
     ctx.set_option("max_cpu_time", 20.0 if cfg == "E" else 0.0)
     try:
