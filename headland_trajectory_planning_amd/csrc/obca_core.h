@@ -3560,21 +3560,32 @@ struct ObcaSolver {
   }
   HTP_HD HTP_FI void grad_lag_into(gd* out) { grad_lag_at(A(L.x), A(L.yc), A(L.yd), A(L.gf), out); }
 
-  HTP_HD HTP_PHASE Err errors(const gd* gl, double mu_) const {
+  // e2 (optional): the same errors at a second barrier parameter mu2, from the same sweeps -- iterate() needs the
+  // mu = 0 optimality errors and the barrier errors at the current mu of one point; only comp depends on mu
+  HTP_HD HTP_PHASE Err errors(const gd* gl, double mu_, double mu2 = 0.0, Err* e2 = nullptr) const {
     const gd* x = A(L.x); const gd* xL = A(L.xL); const gd* xU = A(L.xU);
     const gd* zL = A(L.zL); const gd* zU = A(L.zU);
     const gd* s = A(L.s); const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     const gd* vL = A(L.vL); const gd* vU = A(L.vU);
     const gd* yc = A(L.yc); const gd* yd = A(L.yd);
     const gd* cc = A(L.c); const gd* dd = A(L.d);
-    double dual = 0, comp = 0, zsum = 0, ysum = 0, pb = 0, pn = 0;
+    double dual = 0, comp = 0, comp2 = 0, zsum = 0, ysum = 0, pb = 0, pn = 0;
+    const bool two = e2 != nullptr;
     {
       double g_[SW_U], zl_[SW_U], zu_[SW_U], x_[SW_U], xl_[SW_U], xu_[SW_U];
       sweep(D.n, [&](int q, int k) { g_[k] = gl[q]; zl_[k] = zL[q]; zu_[k] = zU[q]; x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; },
             [&](int, int k) {
               dual = dmax(dual, dabs(g_[k] - zl_[k] + zu_[k]));
-              if (finite_(xl_[k])) { comp = dmax(comp, dabs((x_[k] - xl_[k]) * zl_[k] - mu_)); zsum += dabs(zl_[k]); }
-              if (finite_(xu_[k])) { comp = dmax(comp, dabs((xu_[k] - x_[k]) * zu_[k] - mu_)); zsum += dabs(zu_[k]); }
+              if (finite_(xl_[k])) {
+                comp = dmax(comp, dabs((x_[k] - xl_[k]) * zl_[k] - mu_));
+                if (two) comp2 = dmax(comp2, dabs((x_[k] - xl_[k]) * zl_[k] - mu2));
+                zsum += dabs(zl_[k]);
+              }
+              if (finite_(xu_[k])) {
+                comp = dmax(comp, dabs((xu_[k] - x_[k]) * zu_[k] - mu_));
+                if (two) comp2 = dmax(comp2, dabs((xu_[k] - x_[k]) * zu_[k] - mu2));
+                zsum += dabs(zu_[k]);
+              }
             });
     }
     {
@@ -3583,8 +3594,13 @@ struct ObcaSolver {
             [&](int, int k) {
               dual = dmax(dual, dabs(-yd_[k] - vl_[k] + vu_[k]));
               comp = dmax(comp, dabs((s_[k] - dl_[k]) * vl_[k] - mu_));
+              if (two) comp2 = dmax(comp2, dabs((s_[k] - dl_[k]) * vl_[k] - mu2));
               zsum += dabs(vl_[k]);
-              if (finite_(du_[k])) { comp = dmax(comp, dabs((du_[k] - s_[k]) * vu_[k] - mu_)); zsum += dabs(vu_[k]); }
+              if (finite_(du_[k])) {
+                comp = dmax(comp, dabs((du_[k] - s_[k]) * vu_[k] - mu_));
+                if (two) comp2 = dmax(comp2, dabs((du_[k] - s_[k]) * vu_[k] - mu2));
+                zsum += dabs(vu_[k]);
+              }
               ysum += dabs(yd_[k]);
               pb = dmax(pb, dabs(d_[k] - s_[k]));
               double v = dmax(0.0, dl_[k] - d_[k]);
@@ -3607,6 +3623,7 @@ struct ObcaSolver {
       for (int j = c.lane; j < nR; j += c.width) {
         dual = dmax(dual, dabs(rho + np_jty(j, yc, yd) - zR[j]));
         comp = dmax(comp, dabs(R[j] * zR[j] - mu_));
+        if (two) comp2 = dmax(comp2, dabs(R[j] * zR[j] - mu2));
         zsum += dabs(zR[j]);
       }
     }
@@ -3620,6 +3637,10 @@ struct ObcaSolver {
     const int nz = nbL + nbU + nsL + nsU + (rs ? nR : 0), ny = D.mc + D.md;
     e.s_d = dmax(o.s_max, (ysum + zsum) / (double)(ny + nz > 0 ? ny + nz : 1)) / o.s_max;
     e.s_c = dmax(o.s_max, zsum / (double)(nz > 0 ? nz : 1)) / o.s_max;
+    if (two) {
+      *e2 = e;
+      e2->comp = c.maxv(comp2);
+    }
     return e;
   }
 
@@ -4709,7 +4730,8 @@ struct ObcaSolver {
     for (;;) {
       long long tq0 = c.clock();
       grad_lag_into(gl);
-      Err e0 = errors(gl, 0.0);
+      Err emu;  // errors at the current mu, from the same sweeps (the first barrier test below)
+      Err e0 = errors(gl, 0.0, mu, &emu);
       HTP_TRACE("[trace] it %d%s err dual=%g comp=%g prim=%g mu=%g\n", it, rs ? " R" : "", e0.dual, e0.comp, e0.prim_nlp, mu);
       nlp_err = dmax(dmax(e0.dual / e0.s_d, e0.prim_nlp), e0.comp / e0.s_c);
       const double uv = unscaled_viol();
@@ -4749,8 +4771,8 @@ struct ObcaSolver {
       rs_first = false;
       // monotone barrier update (a tiny step forces a decrease)
       bool stop_tiny = false;
-      for (;;) {
-        Err eb = errors(gl, mu);
+      for (bool first = true;; first = false) {
+        Err eb = first ? emu : errors(gl, mu);
         const double berr = dmax(dmax(eb.dual / eb.s_d, eb.prim_b), eb.comp / eb.s_c);
         if (berr > o.kappa_eps * mu && !ls_.tiny_flag) break;
         const double nm = dmax(o.tol / 10.0, dmin(o.kappa_mu * mu, pow(mu, o.theta_mu)));
