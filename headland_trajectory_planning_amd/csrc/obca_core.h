@@ -3368,12 +3368,9 @@ struct ObcaSolver {
   }
   HTP_HD HTP_FI void compute_eR(bool ls, double dw) {
     gd* eR = A(L.eR);
-    for (int r = c.lane; r < D.mc + D.md; r += c.width) {
-      const int j = r < D.mc ? r : r + D.mc;       // n index of row r
-      double sn, sp;
-      np_diag(j, ls, dw, sn, sp);
-      eR[r] = 1.0 / sn + 1.0 / sp;
-    }
+    double sn_[SW_U], sp_[SW_U];
+    sweep(D.mc + D.md, [&](int r, int k) { np_diag(r < D.mc ? r : r + D.mc, ls, dw, sn_[k], sp_[k]); },  // n index of row r
+          [&](int r, int k) { eR[r] = 1.0 / sn_[k] + 1.0 / sp_[k]; });
     c.sync();
   }
 
@@ -3383,13 +3380,19 @@ struct ObcaSolver {
     const long long t0 = c.clock();
     if (rs) {  // fold the n/p right-hand sides into the constraint rows
       gd* fc = A(L.rcf); gd* fd = A(L.rdf);
-      for (int r = c.lane; r < D.mc + D.md; r += c.width) {
-        const int j = r < D.mc ? r : r + D.mc, jp = r < D.mc ? r + D.mc : r + D.mc + D.md;
-        double sn, sp;
-        np_diag(j, ls, dw, sn, sp);
-        if (r < D.mc) fc[r] = bc[r] - bR[j] / sn + bR[jp] / sp;
-        else fd[r - D.mc] = bd[r - D.mc] - bR[j] / sn + bR[jp] / sp;
-      }
+      double sn_[SW_U], sp_[SW_U], b_[SW_U], bn_[SW_U], bp_[SW_U];
+      sweep(D.mc + D.md, [&](int r, int k) {
+              const int j = r < D.mc ? r : r + D.mc, jp = r < D.mc ? r + D.mc : r + D.mc + D.md;
+              np_diag(j, ls, dw, sn_[k], sp_[k]);
+              b_[k] = r < D.mc ? bc[r] : bd[r - D.mc];
+              bn_[k] = bR[j];
+              bp_[k] = bR[jp];
+            },
+            [&](int r, int k) {
+              const double v = b_[k] - bn_[k] / sn_[k] + bp_[k] / sp_[k];
+              if (r < D.mc) fc[r] = v;
+              else fd[r - D.mc] = v;
+            });
       c.sync();
       bc = fc;
       bd = fd;
@@ -3505,14 +3508,19 @@ struct ObcaSolver {
     c.sync();
     HTP_KPROF(2, tk);
     if (rs) {  // dn = (b_n - dy) / (S_n + dw), dp = (b_p + dy) / (S_p + dw)
-      for (int r = c.lane; r < D.mc + D.md; r += c.width) {
-        const int j = r < D.mc ? r : r + D.mc, jp = r < D.mc ? r + D.mc : r + D.mc + D.md;
-        double sn, sp;
-        np_diag(j, ls, dw, sn, sp);
-        const double dy = r < D.mc ? oc[r] : od[r - D.mc];
-        oR[j] = (bR[j] - dy) / sn;
-        oR[jp] = (bR[jp] + dy) / sp;
-      }
+      double sn_[SW_U], sp_[SW_U], dy_[SW_U], bn_[SW_U], bp_[SW_U];
+      sweep(D.mc + D.md, [&](int r, int k) {
+              const int j = r < D.mc ? r : r + D.mc, jp = r < D.mc ? r + D.mc : r + D.mc + D.md;
+              np_diag(j, ls, dw, sn_[k], sp_[k]);
+              dy_[k] = r < D.mc ? oc[r] : od[r - D.mc];
+              bn_[k] = bR[j];
+              bp_[k] = bR[jp];
+            },
+            [&](int r, int k) {
+              const int j = r < D.mc ? r : r + D.mc, jp = r < D.mc ? r + D.mc : r + D.mc + D.md;
+              oR[j] = (bn_[k] - dy_[k]) / sn_[k];
+              oR[jp] = (bp_[k] + dy_[k]) / sp_[k];
+            });
       c.sync();
     }
     cyc[3] += c.clock() - t0;
@@ -3620,12 +3628,14 @@ struct ObcaSolver {
     if (rs) {  // n/p: rho + J_R'y - z_R, complementarity R z_R
       const gd* R = A(L.R); const gd* zR = A(L.zR);
       const double rho = o.resto_penalty_parameter;
-      for (int j = c.lane; j < nR; j += c.width) {
-        dual = dmax(dual, dabs(rho + np_jty(j, yc, yd) - zR[j]));
-        comp = dmax(comp, dabs(R[j] * zR[j] - mu_));
-        if (two) comp2 = dmax(comp2, dabs(R[j] * zR[j] - mu2));
-        zsum += dabs(zR[j]);
-      }
+      double jt_[SW_U], r_[SW_U], z_[SW_U];
+      sweep(nR, [&](int j, int k) { jt_[k] = np_jty(j, yc, yd); r_[k] = R[j]; z_[k] = zR[j]; },
+            [&](int, int k) {
+              dual = dmax(dual, dabs(rho + jt_[k] - z_[k]));
+              comp = dmax(comp, dabs(r_[k] * z_[k] - mu_));
+              if (two) comp2 = dmax(comp2, dabs(r_[k] * z_[k] - mu2));
+              zsum += dabs(z_[k]);
+            });
     }
     Err e;
     e.dual = c.maxv(dual);
@@ -3692,10 +3702,17 @@ struct ObcaSolver {
     double v = 0;
     if (rs) {
       const gd* dL = A(L.dL); const gd* dU = A(L.dU);
-      for (int r = c.lane; r < D.mc; r += c.width) v = dmax(v, dabs(cc[r]));
-      for (int r = c.lane; r < D.md; r += c.width) {
-        v = dmax(v, dL[r] - dd[r]);
-        if (finite_(dU[r])) v = dmax(v, dd[r] - dU[r]);
+      {
+        double c_[SW_U];
+        sweep(D.mc, [&](int r, int k) { c_[k] = cc[r]; }, [&](int, int k) { v = dmax(v, dabs(c_[k])); });
+      }
+      {
+        double l_[SW_U], d_[SW_U], u_[SW_U];
+        sweep(D.md, [&](int r, int k) { l_[k] = dL[r]; d_[k] = dd[r]; u_[k] = dU[r]; },
+              [&](int, int k) {
+                v = dmax(v, l_[k] - d_[k]);
+                if (finite_(u_[k])) v = dmax(v, d_[k] - u_[k]);
+              });
       }
       return c.maxv(v);
     }
@@ -3734,15 +3751,31 @@ struct ObcaSolver {
   HTP_HD HTP_FI double orig_inf_max_rs(const gd* cc, const gd* dd, const gd* s, const gd* R) const {
     const int mc = D.mc, md = D.md;
     double t = 0;
-    for (int r = c.lane; r < mc; r += c.width) t = dmax(t, dabs(cc[r] - R[r] + R[mc + r]));
-    for (int r = c.lane; r < md; r += c.width) t = dmax(t, dabs(dd[r] - R[2 * mc + r] + R[2 * mc + md + r] - s[r]));
+    {
+      double c_[SW_U], n_[SW_U], p_[SW_U];
+      sweep(mc, [&](int r, int k) { c_[k] = cc[r]; n_[k] = R[r]; p_[k] = R[mc + r]; },
+            [&](int, int k) { t = dmax(t, dabs(c_[k] - n_[k] + p_[k])); });
+    }
+    {
+      double d_[SW_U], n_[SW_U], p_[SW_U], s_[SW_U];
+      sweep(md, [&](int r, int k) { d_[k] = dd[r]; n_[k] = R[2 * mc + r]; p_[k] = R[2 * mc + md + r]; s_[k] = s[r]; },
+            [&](int, int k) { t = dmax(t, dabs(d_[k] - n_[k] + p_[k] - s_[k])); });
+    }
     return c.maxv(t);
   }
   HTP_HD HTP_FI double orig_theta_rs(const gd* cc, const gd* dd, const gd* s, const gd* R) const {
     const int mc = D.mc, md = D.md;
     double t = 0;
-    for (int r = c.lane; r < mc; r += c.width) t += dabs(cc[r] - R[r] + R[mc + r]);
-    for (int r = c.lane; r < md; r += c.width) t += dabs(dd[r] - R[2 * mc + r] + R[2 * mc + md + r] - s[r]);
+    {
+      double c_[SW_U], n_[SW_U], p_[SW_U];
+      sweep(mc, [&](int r, int k) { c_[k] = cc[r]; n_[k] = R[r]; p_[k] = R[mc + r]; },
+            [&](int, int k) { t += dabs(c_[k] - n_[k] + p_[k]); });
+    }
+    {
+      double d_[SW_U], n_[SW_U], p_[SW_U], s_[SW_U];
+      sweep(md, [&](int r, int k) { d_[k] = dd[r]; n_[k] = R[2 * mc + r]; p_[k] = R[2 * mc + md + r]; s_[k] = s[r]; },
+            [&](int, int k) { t += dabs(d_[k] - n_[k] + p_[k] - s_[k]); });
+    }
     return c.sum(t);
   }
 
@@ -3769,12 +3802,20 @@ struct ObcaSolver {
       const gd* xR = A(L.xR); const gd* dr = A(L.dr);
       const double et = o.resto_proximity_weight * sqrt(mu_);
       double px = 0.0, sr = 0.0;
-      for (int q = c.lane; q < D.n; q += c.width) { const double t = dr[q] * (x[q] - xR[q]); px += t * t; }
-      for (int j = c.lane; j < nR; j += c.width) {
-        const double v = Rv[j];
-        if (v <= 0) bad = 1; else lg += log(v);
-        lin += v;
-        sr += v;
+      {
+        double d_[SW_U], x_[SW_U], r_[SW_U];
+        sweep(D.n, [&](int q, int k) { d_[k] = dr[q]; x_[k] = x[q]; r_[k] = xR[q]; },
+              [&](int, int k) { const double t = d_[k] * (x_[k] - r_[k]); px += t * t; });
+      }
+      {
+        double v_[SW_U];
+        sweep(nR, [&](int j, int k) { v_[k] = Rv[j]; },
+              [&](int, int k) {
+                const double v = v_[k];
+                if (v <= 0) bad = 1; else lg += log(v);
+                lin += v;
+                sr += v;
+              });
       }
       fobj = o.resto_penalty_parameter * c.sum(sr) + 0.5 * et * c.sum(px);
     }
@@ -3800,7 +3841,9 @@ struct ObcaSolver {
   // restoration objective gradient (x part): eta D_R^2 (x - x_R)
   HTP_HD HTP_FI void eval_grad_f_rs(const gd* x, gd* g) const {
     const gd* xR = A(L.xR); const gd* dr = A(L.dr);
-    for (int q = c.lane; q < D.n; q += c.width) g[q] = eta * dr[q] * dr[q] * (x[q] - xR[q]);
+    double d_[SW_U], x_[SW_U], r_[SW_U];
+    sweep(D.n, [&](int q, int k) { d_[k] = dr[q]; x_[k] = x[q]; r_[k] = xR[q]; },
+          [&](int q, int k) { g[q] = eta * d_[k] * d_[k] * (x_[k] - r_[k]); });
     c.sync();
   }
   HTP_HD HTP_FI void eval_grad_mode(const gd* x) {
@@ -3876,8 +3919,9 @@ struct ObcaSolver {
     }
     if (rs) {
       const gd* R = A(L.R);
-      for (int j = c.lane; j < nR; j += c.width)
-        if (dR[j] < 0) a = dmin(a, -tau * R[j] / dR[j]);
+      double r_[SW_U], d_[SW_U];
+      sweep(nR, [&](int j, int k) { r_[k] = R[j]; d_[k] = dR[j]; },
+            [&](int, int k) { if (d_[k] < 0) a = dmin(a, -tau * r_[k] / d_[k]); });
     }
     return c.minv(a);
   }
@@ -3917,11 +3961,13 @@ struct ObcaSolver {
     if (rs) {
       const gd* R = A(L.R); const gd* zR = A(L.zR);
       gd* dzR = A(L.dzR);
-      for (int j = c.lane; j < nR; j += c.width) {
-        const double t = (mu - zR[j] * R[j] - zR[j] * dR[j]) / R[j];
-        if (t < 0) a = dmin(a, -tau * zR[j] / t);
-        dzR[j] = t;
-      }
+      double z_[SW_U], r_[SW_U], d_[SW_U];
+      sweep(nR, [&](int j, int k) { z_[k] = zR[j]; r_[k] = R[j]; d_[k] = dR[j]; },
+            [&](int j, int k) {
+              const double t = (mu - z_[k] * r_[k] - z_[k] * d_[k]) / r_[k];
+              if (t < 0) a = dmin(a, -tau * z_[k] / t);
+              dzR[j] = t;
+            });
     }
     c.sync();
     return c.minv(a);
@@ -4076,7 +4122,8 @@ struct ObcaSolver {
     if (rs) {
       const gd* R = A(L.R);
       gd* Rt = A(L.Rt);
-      for (int j = c.lane; j < nR; j += c.width) Rt[j] = R[j] + alpha * dR[j];
+      double r_[SW_U], d_[SW_U];
+      sweep(nR, [&](int j, int k) { r_[k] = R[j]; d_[k] = dR[j]; }, [&](int j, int k) { Rt[j] = r_[k] + alpha * d_[k]; });
     }
     c.sync();
   }
@@ -4227,7 +4274,10 @@ struct ObcaSolver {
     if (rs) {
       const gd* R = A(L.R); const gd* yc = A(L.yc);
       gd* rR = A(L.rRx);
-      for (int j = c.lane; j < nR; j += c.width) rR[j] = -(np_grad_barrier(j, R, mu) + np_jty(j, yc, A(L.yd)));
+      const gd* yd_ = A(L.yd);
+      double b_[SW_U], t_[SW_U];
+      sweep(nR, [&](int j, int k) { b_[k] = np_grad_barrier(j, R, mu); t_[k] = np_jty(j, yc, yd_); },
+            [&](int j, int k) { rR[j] = -(b_[k] + t_[k]); });
     }
     c.sync();
   }
@@ -4242,7 +4292,9 @@ struct ObcaSolver {
     }
     if (rs) {
       const gd* R = A(L.R);
-      for (int j = c.lane; j < nR; j += c.width) g += np_grad_barrier(j, R, mu) * dR[j];
+      double b_[SW_U], d_[SW_U];
+      sweep(nR, [&](int j, int k) { b_[k] = np_grad_barrier(j, R, mu); d_[k] = dR[j]; },
+            [&](int, int k) { g += b_[k] * d_[k]; });
     }
     return c.sum(g);
   }
@@ -4310,12 +4362,14 @@ struct ObcaSolver {
     if (rs) {
       gd* R = A(L.R); gd* zR = A(L.zR);
       const gd* dzR = A(L.dzR);
-      for (int j = c.lane; j < nR; j += c.width) {
-        const double rn = R[j] + a_primal * dR[j];
-        R[j] = rn;
-        const double z = zR[j] + a_dual * dzR[j];
-        zR[j] = dmax(dmin(z, ks * mu / rn), mu / (ks * rn));
-      }
+      double r_[SW_U], d_[SW_U], z_[SW_U], dz_[SW_U];
+      sweep(nR, [&](int j, int k) { r_[k] = R[j]; d_[k] = dR[j]; z_[k] = zR[j]; dz_[k] = dzR[j]; },
+            [&](int j, int k) {
+              const double rn = r_[k] + a_primal * d_[k];
+              R[j] = rn;
+              const double z = z_[k] + a_dual * dz_[k];
+              zR[j] = dmax(dmin(z, ks * mu / rn), mu / (ks * rn));
+            });
     }
     c.sync();
     copy_arr(A(L.c), A(L.ct), D.mc);
@@ -4327,19 +4381,32 @@ struct ObcaSolver {
     if (o.tiny_step_tol == 0.0) return false;
     const gd* x = A(L.x); const gd* s = A(L.s); const gd* cc = A(L.c); const gd* dd = A(L.d);
     double mx = 0.0, ms = 0.0, my = 0.0, pv = 0.0;
-    for (int q = c.lane; q < D.n; q += c.width) mx = dmax(mx, dabs(dx[q]) / (1.0 + dabs(x[q])));
-    if (rs) {
-      const gd* R = A(L.R);
-      for (int j = c.lane; j < nR; j += c.width) mx = dmax(mx, dabs(dR[j]) / (1.0 + dabs(R[j])));
+    {
+      double d_[SW_U], x_[SW_U];
+      sweep(D.n, [&](int q, int k) { d_[k] = dx[q]; x_[k] = x[q]; },
+            [&](int, int k) { mx = dmax(mx, dabs(d_[k]) / (1.0 + dabs(x_[k]))); });
+      if (rs) {
+        const gd* R = A(L.R);
+        sweep(nR, [&](int j, int k) { d_[k] = dR[j]; x_[k] = R[j]; },
+              [&](int, int k) { mx = dmax(mx, dabs(d_[k]) / (1.0 + dabs(x_[k]))); });
+      }
     }
-    for (int r = c.lane; r < D.md; r += c.width) {
-      ms = dmax(ms, dabs(ds[r]) / (1.0 + dabs(s[r])));
-      my = dmax(my, dabs(dyd[r]));
-      pv = dmax(pv, dabs(dd[r] - s[r]));
+    {
+      double d_[SW_U], s_[SW_U], y_[SW_U], v_[SW_U];
+      sweep(D.md, [&](int r, int k) { d_[k] = ds[r]; s_[k] = s[r]; y_[k] = dyd[r]; v_[k] = dd[r]; },
+            [&](int, int k) {
+              ms = dmax(ms, dabs(d_[k]) / (1.0 + dabs(s_[k])));
+              my = dmax(my, dabs(y_[k]));
+              pv = dmax(pv, dabs(v_[k] - s_[k]));
+            });
     }
-    for (int r = c.lane; r < D.mc; r += c.width) {
-      my = dmax(my, dabs(dyc[r]));
-      pv = dmax(pv, dabs(cc[r]));
+    {
+      double y_[SW_U], c_[SW_U];
+      sweep(D.mc, [&](int r, int k) { y_[k] = dyc[r]; c_[k] = cc[r]; },
+            [&](int, int k) {
+              my = dmax(my, dabs(y_[k]));
+              pv = dmax(pv, dabs(c_[k]));
+            });
     }
     mx = c.maxv(mx); ms = c.maxv(ms); my = c.maxv(my); pv = c.maxv(pv);
     if (mx > o.tiny_step_tol || ms > o.tiny_step_tol) return false;
