@@ -465,8 +465,8 @@ struct ObcaSolver {
     return f;
   }
   HTP_HD HTP_PHASE double eval_f(const gd* x) const {
-    double f = 0.0;
-    for (int i = c.lane; i < D.N; i += c.width) f += stage_obj(x, i);
+    double f = 0.0, v_[SW_U];
+    sweep(D.N, [&](int i, int k) { v_[k] = stage_obj(x, i); }, [&](int, int k) { f += v_[k]; });
     return c.sum(f);
   }
   // scaled gradient (sf * grad f) into g (all n entries written)
@@ -3855,8 +3855,11 @@ struct ObcaSolver {
     eval_cons(x, cc, dd);
     if (rs) {
       const int mc = D.mc, md = D.md;
-      for (int r = c.lane; r < mc; r += c.width) cc[r] += Rv[r] - Rv[mc + r];
-      for (int r = c.lane; r < md; r += c.width) dd[r] += Rv[2 * mc + r] - Rv[2 * mc + md + r];
+      double v_[SW_U], n_[SW_U], p_[SW_U];
+      sweep(mc, [&](int r, int k) { v_[k] = cc[r]; n_[k] = Rv[r]; p_[k] = Rv[mc + r]; },
+            [&](int r, int k) { cc[r] = v_[k] + (n_[k] - p_[k]); });
+      sweep(md, [&](int r, int k) { v_[k] = dd[r]; n_[k] = Rv[2 * mc + r]; p_[k] = Rv[2 * mc + md + r]; },
+            [&](int r, int k) { dd[r] = v_[k] + (n_[k] - p_[k]); });
       c.sync();
     }
   }
