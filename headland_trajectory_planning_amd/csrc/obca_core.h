@@ -22,8 +22,10 @@
 #ifndef HTP_UNROLL_N
 #define HTP_UNROLL_N 4
 #endif
+// loads in flight per lane in sweep(): 8 and 12 give the fewest cycles per iteration, 4 is 4 % and 2 is 14 % slower,
+// 16 is slower again (profiles/r03t_ab_sweep_unroll.txt, r03u_ab_sweep_unroll.txt; results bit-identical)
 #ifndef HTP_SWEEP_U
-#define HTP_SWEEP_U 4
+#define HTP_SWEEP_U 8
 #endif
 #define HTP_PRAGMA_(x) _Pragma(#x)
 #define HTP_PRAGMA(x) HTP_PRAGMA_(x)
