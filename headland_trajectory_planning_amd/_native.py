@@ -187,7 +187,44 @@ def _declare(lib):
     lib.htp_orchard_chain_device.restype = ctypes.c_int
     lib.htp_chain_last_ms.argtypes = [ctypes.c_void_p]
     lib.htp_chain_last_ms.restype = ctypes.c_double
+    lib.htp_libm_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int32] + [ctypes.c_void_p] * 3 + \
+        [ctypes.c_int64, ctypes.c_void_p]
+    lib.htp_libm_batch_device.restype = ctypes.c_int
     return lib
+
+
+# correctly rounded libm of the planner cores (csrc/htp_libm.h): function ids of htp_libm_batch_device
+LIBM_FN = {"sin": 0, "cos": 1, "tan": 2, "atan": 3, "atan2": 4, "asin": 5, "acos": 6, "hypot": 7, "pow": 8}
+LIBM_BINARY = {"atan2", "hypot", "pow"}
+CPU_LIB_PATH = os.path.join(HERE, "libhtp_cpu.so")
+_CPU_LIB = None
+
+
+def cpu_lib():
+    """libhtp_cpu.so: the g++ build of the same cores (CPU baseline, workload generator, host twins)."""
+    global _CPU_LIB
+    if _CPU_LIB is None:
+        if not os.path.exists(CPU_LIB_PATH):
+            raise RuntimeError(f"[htp] CPU library not built: {CPU_LIB_PATH} (run __graft_entry__.build())")
+        lib = ctypes.CDLL(CPU_LIB_PATH)
+        lib.htp_cpu_libm_batch.argtypes = [ctypes.c_int32] + [ctypes.c_void_p] * 3 + [ctypes.c_int64]
+        lib.htp_cpu_libm_batch.restype = ctypes.c_int
+        _CPU_LIB = lib
+    return _CPU_LIB
+
+
+def cpu_libm(name, x, y=None):
+    """Host build of the planner libm: name in LIBM_FN, x (and y) float64 arrays -> float64 array."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    yy = np.ascontiguousarray(np.broadcast_to(y, x.shape), dtype=np.float64) if y is not None else None
+    if name in LIBM_BINARY and yy is None:
+        raise ValueError(f"[htp] {name} needs two arguments")
+    out = np.empty_like(x)
+    rc = cpu_lib().htp_cpu_libm_batch(LIBM_FN[name], x.ctypes.data, yy.ctypes.data if yy is not None else None,
+                                      out.ctypes.data, x.size)
+    if rc != 0:
+        raise RuntimeError("[htp] htp_cpu_libm_batch failed")
+    return out
 
 
 _LIB = None
@@ -856,6 +893,24 @@ class Context:
         if rc != 0:
             raise RuntimeError(f"[htp] htp_obca_solve_batch failed: {self.error()}")
         return res
+
+    def libm(self, name, x, y=None):
+        """The device build of the planner libm over host arrays (through device buffers) -> float64 array."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        xt = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64)).to(dev)
+        yt = None
+        if y is not None:
+            yt = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(y, np.shape(x)), dtype=np.float64)).to(dev)
+        out = torch.empty_like(xt)
+        s = torch.cuda.current_stream(dev)
+        rc = self.lib.htp_libm_batch_device(self.ctx, LIBM_FN[name], xt.data_ptr(),
+                                            yt.data_ptr() if yt is not None else None, out.data_ptr(), xt.numel(),
+                                            ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"[htp] htp_libm_batch_device failed: {self.error()}")
+        s.synchronize()
+        return out.cpu().numpy()
 
     def solve_points(self, packed):
         """Batched optimizer_points.py solve (host buffers)."""

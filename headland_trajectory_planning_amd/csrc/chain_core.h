@@ -5,7 +5,7 @@
 //
 //   prep ..... the turn's length (np.sum of np.hypot of the path steps: numpy's pairwise summation),
 //              ds = L / (N - 1), desired_v = min(ds / dT, 0.9): get_init_ref_path's inputs
-//              (R/obca_py/util.py:62-113 at spacing L / (2 N - 1.5))
+//              (R/obca_py/util.py:62-113 at spacing ds / 2 = L / (2 N - 2))
 //   resample . the init guess at N rows of even arc length (synth._resample_rows) and the headland width
 //              the warm start needs (synth._needed_headland over the footprint of both pose sets):
 //              max(6, needed + margin) -> the orchard producer's headland_width
@@ -15,6 +15,7 @@
 // Sequential pieces run on lane 0 (they are short); results are written once per problem.
 #pragma once
 #include <cmath>
+#include "htp_libm.h"
 #include <cstdint>
 
 #include "oge_core.h"
@@ -81,7 +82,7 @@ struct Vehicle {             // car-frame polygons of the footprint (body, then 
 
 // the polygon `k` of the vehicle placed at pose (x, y, th) (synth._polys_at arithmetic)
 HTP_HD inline void place(const Vehicle& V, int k, double x, double y, double th, double* px, double* py) {
-  const double c = cos(th), s = sin(th);
+  const double c = hm::cos(th), s = hm::sin(th);
   for (int j = 0; j < V.nv[k]; ++j) {
     px[j] = V.v[k][j][0] * c - V.v[k][j][1] * s + x;
     py[j] = V.v[k][j][0] * s + V.v[k][j][1] * c + y;
@@ -135,13 +136,13 @@ HTP_HD inline void prep(const double* rows, int n, int N, double dT, double wb, 
     ys[i] = rows[5 * i + 1];
     dirs[i] = rows[5 * i + 4];
   }
-  for (int i = 0; i + 1 < n; ++i) steps[i] = hypot(rows[5 * (i + 1)] - rows[5 * i], rows[5 * (i + 1) + 1] - rows[5 * i + 1]);
+  for (int i = 0; i + 1 < n; ++i) steps[i] = hm::hypot(rows[5 * (i + 1)] - rows[5 * i], rows[5 * (i + 1) + 1] - rows[5 * i + 1]);
   const double Lp = pairwise_sum(steps, n - 1);
   const double ds = Lp / (N - 1);
   const double dv = ds / dT;
   rp_params[0] = wb;
   rp_params[1] = dv < 0.9 ? dv : 0.9;   // min(ds / dT, 0.9)
-  rp_params[2] = Lp / (2.0 * N - 1.5);   // synth: off the integer sample-count boundary of a one-gear turn
+  rp_params[2] = Lp / (2.0 * N - 2.0);   // ds / 2 (synth.make_orchard_instance)
 }
 
 // ---- resample (synth._resample_rows) + the headland width the warm start needs (lane 0)
@@ -149,7 +150,7 @@ HTP_HD inline void prep(const double* rows, int n, int N, double dT, double wb, 
 HTP_HD inline double resample_hw(const double* ref, int nr, int N, double* s, double* traj, const Vehicle& V,
                                  const oge::Scene& S, double margin) {
   s[0] = 0.0;
-  for (int i = 1; i < nr; ++i) s[i] = s[i - 1] + hypot(ref[5 * i] - ref[5 * (i - 1)], ref[5 * i + 1] - ref[5 * (i - 1) + 1]);
+  for (int i = 1; i < nr; ++i) s[i] = s[i - 1] + hm::hypot(ref[5 * i] - ref[5 * (i - 1)], ref[5 * i + 1] - ref[5 * (i - 1) + 1]);
   const double send = s[nr - 1];
   const double tstep = send / (N - 1);
   for (int k = 0; k < N; ++k) {
@@ -192,7 +193,7 @@ HTP_HD inline double resample_hw(const double* ref, int nr, int N, double* s, do
       }
     }
   }
-  const double nh = need * fabs(sin(ang)) + margin;
+  const double nh = need * fabs(hm::sin(ang)) + margin;
   return nh > 6.0 ? nh : 6.0;
 }
 

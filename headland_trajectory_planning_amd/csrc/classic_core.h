@@ -20,6 +20,7 @@
 // tridiagonal solve, cumulative sums) run on one lane, as the reference runs them.
 #pragma once
 #include <cmath>
+#include "htp_libm.h"
 #include <cstdint>
 
 #include "hastar_core.h"
@@ -59,7 +60,7 @@ struct Turn {
   int* flags;          // MAXP ints (wave-shared)
   int n_out = 0, status = ST_OK;
 
-  HTP_HD double curvature() const { return tan(sp.max_steer) / sp.wb; }   // car_model.py:34
+  HTP_HD double curvature() const { return hm::tan(sp.max_steer) / sp.wb; }   // car_model.py:34
 
   HTP_HD void put_row(int r, double x, double y, double yaw, double k, double d) {
     double* o = out + 5 * (int64_t)r;
@@ -107,14 +108,15 @@ struct Turn {
       }
       for (int i = 0; i < m; ++i) { X[i] = T[i]; Y[i] = WK[i]; }
       S[0] = 0.0;
-      for (int i = 1; i < m; ++i) S[i] = S[i - 1] + hypot(X[i] - X[i - 1], Y[i] - Y[i - 1]);
+      for (int i = 1; i < m; ++i) S[i] = S[i - 1] + hm::hypot(X[i] - X[i - 1], Y[i] - Y[i - 1]);
     }
     m = c.uniform_i(m);
     c.sync();
     if (m < 2) { status = ST_NO_DUBINS; return -1; }
     if (c.lane == 0 || C::width == 1) dub::spline_slopes(S, X, m, DX, WK);
     c.sync();
-    if (c.lane == (C::width > 1 ? 1 : 0)) dub::spline_slopes(S, Y, m, DY, T);   // T reused as work (4m <= 4 cap)
+    // WK (4 cap_scr doubles) is free again once the X solve has finished: the Y solve uses it too
+    if (c.lane == (C::width > 1 ? 1 : 0)) dub::spline_slopes(S, Y, m, DY, WK);
     c.sync();
     const double ds = 0.1;
     const double nsd = ceil((S[m - 1] + ds) / ds);
@@ -128,8 +130,8 @@ struct Turn {
       double x, x1, x2, y, y1, y2;
       dub::eval3(S, X, DX, iv, v, x, x1, x2);
       dub::eval3(S, Y, DY, iv, v, y, y1, y2);
-      const double kap = (y2 * x1 - x2 * y1) / pow(x1 * x1 + y1 * y1, 1.5);
-      put_row(row0 + k - k0, x, y, atan2(y1, x1), kap, 1.0);
+      const double kap = (y2 * x1 - x2 * y1) / hm::pow(x1 * x1 + y1 * y1, 1.5);
+      put_row(row0 + k - k0, x, y, hm::atan2(y1, x1), kap, 1.0);
     }
     c.sync();
     return k1 - k0;
@@ -138,23 +140,23 @@ struct Turn {
   // calculate_motion_path_new(init_pose, motion_dir, steer_dir, turning_radius, delta_yaw, step) car_model.py:236-269
   HTP_HD int arc_new(const double* p0, double mdir, double sdir, double R, double dyaw, double step, int row0) {
     const double tr = fmax(1.0 / curvature(), R);
-    const double steer = atan(sp.wb / tr) * sdir;
+    const double steer = hm::atan(sp.wb / tr) * sdir;
     const double arc = fabs(dyaw * tr);
     const int num = (int)(arc / step);
     if (num < 1) { status = ST_BAD_INPUT; return -1; }
     const double act = arc / num;
-    const double ystep = mdir * act / sp.wb * tan(steer);
+    const double ystep = mdir * act / sp.wb * hm::tan(steer);
     const double iy = wrap(p0[2]);
     const double stop = iy + ystep * num;
     const double lstep = (stop - iy) / num;
-    const double kap = fabs(steer) > 0.00001 ? tan(steer) / sp.wb : 0.0;
+    const double kap = fabs(steer) > 0.00001 ? hm::tan(steer) / sp.wb : 0.0;
     if (row0 + num + 2 > cap_out) { status = ST_OVERFLOW; return -1; }
     if (c.lane == 0) put_row(row0, p0[0], p0[1], p0[2], kap, mdir);
     for (int k = c.lane; k <= num; k += C::width) {
       const double yl = k == num ? stop : (double)k * lstep + iy;   // np.linspace
       const double yaw = wrap(yl);
-      const double x = p0[0] + tr * (sin(yaw) - sin(iy)) * sdir;
-      const double y = p0[1] - tr * (cos(yaw) - cos(iy)) * sdir;
+      const double x = p0[0] + tr * (hm::sin(yaw) - hm::sin(iy)) * sdir;
+      const double y = p0[1] - tr * (hm::cos(yaw) - hm::cos(iy)) * sdir;
       put_row(row0 + 1 + k, x, y, yaw, kap, mdir);
     }
     c.sync();
@@ -162,7 +164,7 @@ struct Turn {
   }
 
   HTP_HD static double enter_steer_dir(const double* s, const double* e) {   // :37-45
-    return e[1] - s[1] > 0 ? sgnf(1.0 * cos(s[2])) : sgnf(-1.0 * cos(s[2]));
+    return e[1] - s[1] > 0 ? sgnf(1.0 * hm::cos(s[2])) : sgnf(-1.0 * hm::cos(s[2]));
   }
 
   // get_offset_pose (:248-283): first dist = 0, 0.1, ... 5 whose 45-degree arc clears the blockers
@@ -171,14 +173,14 @@ struct Turn {
     const double st = 0.55 * turn_dir, step = 0.1, dyaw = 0.7853981633974483;   // math.radians(45)
     const double search_len = dyaw / curvature();
     const int num = (int)rint(search_len / step);
-    const double ystep = mdir * step / sp.wb * tan(st);
+    const double ystep = mdir * step / sp.wb * hm::tan(st);
     double* PX = scr;
     double* PY = scr + cap_scr;
     double* PW = scr + 2 * cap_scr;
     if (num + 1 > cap_scr) { status = ST_OVERFLOW; return; }
     for (int kd = 0; kd < 51; ++kd) {   // np.arange(0, max_offset + accuracy, accuracy)
       const double dist = 0.0 + (double)kd * 0.1;
-      const double x0 = init[0] + dist * cos(init[2]) * odir, y0 = init[1] + dist * sin(init[2]) * odir;
+      const double x0 = init[0] + dist * hm::cos(init[2]) * odir, y0 = init[1] + dist * hm::sin(init[2]) * odir;
       pose[0] = x0; pose[1] = y0; pose[2] = init[2];
       if (c.lane == 0 || C::width == 1) {   // calculate_motion_path :202-234 (sequential cumsum)
         const double iy = wrap(init[2] + ystep);
@@ -187,8 +189,8 @@ struct Turn {
         PX[0] = x0; PY[0] = y0; PW[0] = init[2];
         double cx = 0.0, cy = 0.0, prev = wrap(iy);   // np.cumsum of the steps, then added to the pose
         for (int k = 1; k <= num; ++k) {
-          cx = cx + step * cos(prev) * mdir;
-          cy = cy + step * sin(prev) * mdir;
+          cx = cx + step * hm::cos(prev) * mdir;
+          cy = cy + step * hm::sin(prev) * mdir;
           const double yk = wrap(k == num ? stop : (double)k * lstep + iy);
           PX[k] = x0 + cx; PY[k] = y0 + cy; PW[k] = yk;
           prev = yk;
@@ -248,7 +250,7 @@ struct Turn {
       if (n < 0) {
         f = -1;
       } else {
-        CheckSink ck{&fp, so[0], so[1], so[2], cos(-so[2]), sin(-so[2]), n};
+        CheckSink ck{&fp, so[0], so[1], so[2], hm::cos(-so[2]), hm::sin(-so[2]), n};
         rs::local_course(paths[p], maxc, step * maxc, ck);
         ck.test(ck.cur);
         f = ck.hit ? 0 : 1;
@@ -297,7 +299,7 @@ struct Turn {
             r[3] = cv;
             r[4] = (double)d;
           }
-        } rsk{o, n, so[0], so[1], so[2], cos(-so[2]), sin(-so[2])};
+        } rsk{o, n, so[0], so[1], so[2], hm::cos(-so[2]), hm::sin(-so[2])};
         rs::local_course(paths[best], maxc, step * maxc, rsk);
       }
       c.sync();
@@ -323,9 +325,9 @@ struct Turn {
     }
     double Rf = tr, Rb = tr, theta = 0.0;
     for (int it = 0; it < 100000; ++it) {
-      theta = PI / 2 + asin((Rb + w - Rf) / (Rf + Rb));
-      if (sp.side == NEAR_SIDE && s0[0] - (Rf + Rb) * cos(theta - PI / 2) < e0[0] - sp.step) break;
-      if (sp.side == FAR_SIDE && s0[0] + (Rf + Rb) * cos(theta - PI / 2) > e0[0] + sp.step) break;
+      theta = PI / 2 + hm::asin((Rb + w - Rf) / (Rf + Rb));
+      if (sp.side == NEAR_SIDE && s0[0] - (Rf + Rb) * hm::cos(theta - PI / 2) < e0[0] - sp.step) break;
+      if (sp.side == FAR_SIDE && s0[0] + (Rf + Rb) * hm::cos(theta - PI / 2) > e0[0] + sp.step) break;
       Rf *= 1.05;
       Rb *= 1.05;
     }

@@ -25,6 +25,8 @@
 #error "define HTP_HD before including dubins_core.h"
 #endif
 
+#include "htp_libm.h"
+
 namespace htp {
 namespace dub {
 
@@ -51,10 +53,10 @@ HTP_HD inline bool shortest(const double* q0, const double* q1, double rho, Path
   const double dx = q1[0] - q0[0], dy = q1[1] - q0[1];
   const double D = sqrt(dx * dx + dy * dy);
   const double d = D / rho;
-  const double th = d > 0 ? mod2pi(atan2(dy, dx)) : 0.0;
+  const double th = d > 0 ? mod2pi(hm::atan2(dy, dx)) : 0.0;
   const double a = mod2pi(q0[2] - th), b = mod2pi(q1[2] - th);
-  const double sa = sin(a), sb = sin(b), ca = cos(a), cb = cos(b);
-  const double cab = cos(a - b), dd = d * d;
+  const double sa = hm::sin(a), sb = hm::sin(b), ca = hm::cos(a), cb = hm::cos(b);
+  const double cab = hm::cos(a - b), dd = d * d;
   double best = __builtin_huge_val();
   int bw = -1;
   double bp[3] = {0, 0, 0};
@@ -64,37 +66,37 @@ HTP_HD inline bool shortest(const double* q0, const double* q1, double rho, Path
   };
   double p2 = 2 + dd - (2 * cab) + (2 * d * (sa - sb));
   if (p2 >= 0) {
-    const double t1 = atan2(cb - ca, d + sa - sb);
+    const double t1 = hm::atan2(cb - ca, d + sa - sb);
     take(LSL, mod2pi(t1 - a), sqrt(p2), mod2pi(b - t1));
   }
   p2 = -2 + dd + (2 * cab) + (2 * d * (sa + sb));
   if (p2 >= 0) {
     const double p = sqrt(p2);
-    const double t0 = atan2(-ca - cb, d + sa + sb) - atan2(-2.0, p);
+    const double t0 = hm::atan2(-ca - cb, d + sa + sb) - hm::atan2(-2.0, p);
     take(LSR, mod2pi(t0 - a), p, mod2pi(t0 - mod2pi(b)));
   }
   p2 = -2 + dd + (2 * cab) - (2 * d * (sa + sb));
   if (p2 >= 0) {
     const double p = sqrt(p2);
-    const double t0 = atan2(ca + cb, d - sa - sb) - atan2(2.0, p);
+    const double t0 = hm::atan2(ca + cb, d - sa - sb) - hm::atan2(2.0, p);
     take(RSL, mod2pi(a - t0), p, mod2pi(b - t0));
   }
   p2 = 2 + dd - (2 * cab) + (2 * d * (sb - sa));
   if (p2 >= 0) {
-    const double t1 = atan2(ca - cb, d - sa + sb);
+    const double t1 = hm::atan2(ca - cb, d - sa + sb);
     take(RSR, mod2pi(a - t1), sqrt(p2), mod2pi(t1 - b));
   }
   double t0 = (6. - dd + 2 * cab + 2 * d * (sa - sb)) / 8.;
-  double phi = atan2(ca - cb, d - sa + sb);
+  double phi = hm::atan2(ca - cb, d - sa + sb);
   if (fabs(t0) <= 1) {
-    const double p = mod2pi(TWO_PI - acos(t0));
+    const double p = mod2pi(TWO_PI - hm::acos(t0));
     const double t = mod2pi(a - phi + mod2pi(p / 2.));
     take(RLR, t, p, mod2pi(a - b - t + mod2pi(p)));
   }
   t0 = (6. - dd + 2 * cab + 2 * d * (sb - sa)) / 8.;
-  phi = atan2(ca - cb, d + sa - sb);
+  phi = hm::atan2(ca - cb, d + sa - sb);
   if (fabs(t0) <= 1) {
-    const double p = mod2pi(TWO_PI - acos(t0));
+    const double p = mod2pi(TWO_PI - hm::acos(t0));
     const double t = mod2pi(-a - phi + p / 2.);
     take(LRL, t, p, mod2pi(mod2pi(b) - a - t + mod2pi(p)));
   }
@@ -115,9 +117,9 @@ HTP_HD inline double length(const Path& P) {
 }
 
 HTP_HD inline void segment(double t, const double* qi, double* qt, int typ) {
-  const double st = sin(qi[2]), ct = cos(qi[2]);
-  if (typ == SL) { qt[0] = sin(qi[2] + t) - st; qt[1] = -cos(qi[2] + t) + ct; qt[2] = t; }
-  else if (typ == SR) { qt[0] = -sin(qi[2] - t) + st; qt[1] = cos(qi[2] - t) - ct; qt[2] = -t; }
+  const double st = hm::sin(qi[2]), ct = hm::cos(qi[2]);
+  if (typ == SL) { qt[0] = hm::sin(qi[2] + t) - st; qt[1] = -hm::cos(qi[2] + t) + ct; qt[2] = t; }
+  else if (typ == SR) { qt[0] = -hm::sin(qi[2] - t) + st; qt[1] = hm::cos(qi[2] - t) - ct; qt[2] = -t; }
   else { qt[0] = ct * t; qt[1] = st * t; qt[2] = 0.0; }
   qt[0] += qi[0];
   qt[1] += qi[1];

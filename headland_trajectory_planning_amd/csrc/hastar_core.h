@@ -27,6 +27,7 @@
 // Arithmetic follows the reference's expression order; no FMA contraction.
 #pragma once
 #include <cmath>
+#include "htp_libm.h"
 #include <cstdint>
 #ifdef HTP_HA_DEBUG
 #include <cstdio>
@@ -258,7 +259,7 @@ struct Footprint {
   }
 
   HTP_HD bool pose_hits(double x, double y, double yaw) const {
-    const double cs = cos(yaw), sn = sin(yaw);
+    const double cs = hm::cos(yaw), sn = hm::sin(yaw);
     double bx[MAXB], by[MAXB];
     for (int k = 0; k < nb; ++k) {
       const double vx = body[2 * k], vy = body[2 * k + 1];
@@ -345,7 +346,7 @@ struct Search {
     double best = 0.0;
     int bi = -1;
     for (int q = G0 + c.lane; q < G1; q += C::width) {
-      const double d = hypot(g.guide[4 * q] - x, g.guide[4 * q + 1] - y);
+      const double d = hm::hypot(g.guide[4 * q] - x, g.guide[4 * q + 1] - y);
       if (bi < 0 || d < best) { best = d; bi = q; }
     }
     if (bi < 0) { best = __builtin_huge_val(); bi = 0x7fffffff; }
@@ -438,7 +439,7 @@ struct Search {
   // Lane m integrates primitive m from pose (x0, y0, yaw0) with n steps into sh.traj.
   HTP_HD void simulate(int m, double x0, double y0, double yaw0, int n) {
     const double steer = g.motion[2 * (dsc[D_MOT0] + m)], dir = g.motion[2 * (dsc[D_MOT0] + m) + 1];
-    const double yaw_step = dir * res / wb * tan(steer);
+    const double yaw_step = dir * res / wb * hm::tan(steer);
     const double init_yaw = angle_wrap(yaw0 + yaw_step);
     const double stop = init_yaw + yaw_step * (double)(n + 1);
     const int num = n + 2;
@@ -450,8 +451,8 @@ struct Search {
     for (int i = 0; i <= n; ++i) {  // numpy linspace (step == 0 branch included), angle_wrap, cumsum
       const double yi = (step == 0) ? ((double)i / div) * delta + init_yaw : (double)i * step + init_yaw;
       const double wy = angle_wrap(yi);
-      const double dx = res * cos(wy) * dir;
-      const double dy = res * sin(wy) * dir;
+      const double dx = res * hm::cos(wy) * dir;
+      const double dy = res * hm::sin(wy) * dir;
       ax = (i == 0) ? dx : ax + dx;
       ay = (i == 0) ? dy : ay + dy;
       const double ni = (i + 1 == num - 1) ? stop : ((step == 0) ? ((double)(i + 1) / div) * delta + init_yaw
@@ -469,13 +470,13 @@ struct Search {
     double cost = par.cost;
     double pl = 0.0;
     for (int i = 0; i < n; ++i) {
-      const double d = hypot(T[3 * (i + 1)] - T[3 * i], T[3 * (i + 1) + 1] - T[3 * i + 1]);
+      const double d = hm::hypot(T[3 * (i + 1)] - T[3 * i], T[3 * (i + 1) + 1] - T[3 * i + 1]);
       pl = (i == 0) ? d : pl + d;
     }
     cost += pl;
     if (dir == -1) cost += 5000;
     cost += steer * 1;
-    const double sa = atan(par.curv * wb);
+    const double sa = hm::atan(par.curv * wb);
     cost += fabs(steer - sa) * 5;
     if ((double)par.dir != dir) cost += 1000;
     return cost;
@@ -487,11 +488,11 @@ struct Search {
     const double gx = prm[P_GX], gy = prm[P_GY], gyaw = prm[P_GYAW];
     const double maxc = curv_max;
     const double dx = gx - sx, dy = gy - sy, dth = gyaw - syaw;
-    const double cc = cos(syaw), ss = sin(syaw);
+    const double cc = hm::cos(syaw), ss = hm::sin(syaw);
     const double x = (cc * dx + ss * dy) * maxc;
     const double y = (-ss * dx + cc * dy) * maxc;
-    const double xb = x * cos(dth) + y * sin(dth);
-    const double yb = x * sin(dth) - y * cos(dth);
+    const double xb = x * hm::cos(dth) + y * hm::sin(dth);
+    const double yb = x * hm::sin(dth) - y * hm::cos(dth);
     const rs::Cand* T = rs::cand_table();
     for (int k = c.lane; k < 46; k += C::width) {
       const rs::Cand& cd = T[k];
@@ -549,7 +550,7 @@ struct Search {
   // chunks of 64; true if any sample collides.
   HTP_HD bool rs_path_hits(const rs::Path& p, double sx, double sy, double syaw, int64_t& n_pose) {
     const double maxc = curv_max, step = maxc * res;
-    const double cq = cos(-syaw), sq = sin(-syaw);
+    const double cq = hm::cos(-syaw), sq = hm::sin(-syaw);
     // segment origins (the previous segment's end sample, zeros first)
     double ox = 0.0, oy = 0.0, oyaw = 0.0;
     for (int i = 0; i < p.nseg; ++i) {
@@ -742,7 +743,7 @@ struct Search {
     }
     c.sync();
     S[0] = 0.0;
-    for (int i = 1; i < mm; ++i) S[i] = S[i - 1] + hypot(X[i] - X[i - 1], Y[i] - Y[i - 1]);
+    for (int i = 1; i < mm; ++i) S[i] = S[i - 1] + hm::hypot(X[i] - X[i - 1], Y[i] - Y[i - 1]);
     c.sync();
     m = mm;
 #ifdef HTP_HA_DEBUG
@@ -775,8 +776,8 @@ struct Search {
     double x1, x2, y1, y2;
     dub::eval3(S, X, DX, i, v, x, x1, x2);
     dub::eval3(S, Y, DY, i, v, y, y1, y2);
-    yaw = atan2(y1, x1);
-    kap = (y2 * x1 - x2 * y1) / pow(x1 * x1 + y1 * y1, 1.5);
+    yaw = hm::atan2(y1, x1);
+    kap = (y2 * x1 - x2 * y1) / hm::pow(x1 * x1 + y1 * y1, 1.5);
   }
 
   // _get_goal_extension_with_dubins_path :184-230: true if the shot is taken
@@ -799,7 +800,7 @@ struct Search {
     // calculate_path_length: cumsum of hypot(diff) (sequential)
     double len = 0.0;
     for (int k = 1; k < ns; ++k) {
-      const double h = hypot(XS[k] - XS[k - 1], YS[k] - YS[k - 1]);
+      const double h = hm::hypot(XS[k] - XS[k - 1], YS[k] - YS[k - 1]);
       len = (k == 1) ? h : len + h;
     }
     if (!(len < 1000.0)) return false;  // path_length < MIN_LENGTH_TO_GOAL (checked first: same outcome)
@@ -957,7 +958,7 @@ struct Search {
       for (int m = c.lane; m < nmot; m += C::width) {
         sh.ccost[m] = motion_cost(m, n, cur);
         const double steer = g.motion[2 * (dsc[D_MOT0] + m)];
-        sh.ccurv[m] = tan(steer) / wb;
+        sh.ccurv[m] = hm::tan(steer) / wb;
         const double* T = sh.traj + (m * MAXTRAJ + n) * 3;
         index(T[0], T[1], T[2], sh.ckey + 3 * m);
       }
@@ -1042,7 +1043,7 @@ struct Search {
         if (c.lane == 0 || C::width == 1) simulate(nd.aux, par.x, par.y, par.yaw, n);
         c.sync();
         const double dir = g.motion[2 * (dsc[D_MOT0] + nd.aux) + 1];
-        const double kv = tan(g.motion[2 * (dsc[D_MOT0] + nd.aux)]) / wb;
+        const double kv = hm::tan(g.motion[2 * (dsc[D_MOT0] + nd.aux)]) / wb;
         const double* T = sh.traj + nd.aux * MAXTRAJ * 3;
         for (int i = c.lane; i <= n; i += C::width)
           if (off + i < cap_path) {
@@ -1083,8 +1084,8 @@ struct Search {
               cs[kk] = cc;
               dir[kk] = (double)d;
             }
-          } gs{px + off, py + off, pyaw + off, pk + off, pdir + off, cnt, par.x, par.y, par.yaw, cos(-par.yaw),
-               sin(-par.yaw)};
+          } gs{px + off, py + off, pyaw + off, pk + off, pdir + off, cnt, par.x, par.y, par.yaw, hm::cos(-par.yaw),
+               hm::sin(-par.yaw)};
           rs::local_course(P, curv_max, curv_max * res, gs);
         }
         off += cnt > 0 ? cnt : 0;

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(64) void k_resample(htp_chain_batch in, ChainBufs w
   sc.slope = p[HTP_OGE_P_SLOPE];
   sc.row_draws = in.scenes.row_draws + b * in.scenes.max_rows;
   oge::Scene S;
-  if (sc.nrows < 3 || sc.nrows > in.scenes.max_rows) return;
+  if (sc.nrows < 3 || sc.nrows > in.scenes.max_rows || sc.nrows > oge::MAXR) return;
   oge::make_rows(sc, S);
   const double hw = chain::resample_hw(w.rp_traj + b * (int64_t)in.cap_rows * 5, w.rp_rows[b], in.N,
                                        w.s + b * (int64_t)in.cap_rows, in.traj + b * (int64_t)in.N * 5, V, S,
@@ -145,6 +145,14 @@ int htp_orchard_chain_device(htp_ctx* ctx, const htp_chain_batch* in, void* stre
       (in->n_vpoly == 2 && (in->vpoly_nv[1] < 3 || in->vpoly_nv[1] > 8)))
     return fail(ctx, "chain: vehicle polygons");
   if (!in->traj || !in->obs_A || !in->obs_b || !in->status || !in->margin) return fail(ctx, "chain: output missing");
+  // the stage kernels' own entry checks (htp_oge.hip, htp_classic.hip check_in): k_resample / k_pack build the
+  // scene's rows into fixed [oge::MAXR] arrays, the classic stage needs its scratch and path pools
+  if (in->scenes.max_rows < 3 || in->scenes.max_rows > HTP_OGE_MAXROWS || in->scenes.max_rows > oge::MAXR)
+    return fail(ctx, "chain: scenes.max_rows out of [3, HTP_OGE_MAXROWS]");
+  if (!in->scenes.params || !in->scenes.row_draws || !in->scenes.eps_draws) return fail(ctx, "chain: scene input missing");
+  if (in->turns.cap_samples < 16 || in->turns.cap_path < 2) return fail(ctx, "chain: turns.cap_samples / cap_path");
+  if (!in->turns.params || !in->turns.desc || !in->turns.poly_off || !in->turns.vertices)
+    return fail(ctx, "chain: turn input missing");
   if (B == 0) return 0;
   HIPCHK(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
@@ -157,6 +165,7 @@ int htp_orchard_chain_device(htp_ctx* ctx, const htp_chain_batch* in, void* stre
                          8 * Bz * rp::SCRATCH_PER_POINT * cap, 4 * Bz, 4 * Bz, 40 * Bz * cr, 8 * Bz * cr,
                          4 * Bz * (3 + oge::MAXPOLY), 16 * Bz * oge::MAXPOLY * oge::MAXV};
   for (int k = 0; k < 16; ++k) { off[k] = o; o += al(sz[k]); }
+  if (order_after(ctx, ctx->ch_ev1, s)) return -1;
   if (ensure(ctx, &ctx->ch_ws, &ctx->ch_ws_bytes, o)) return -1;
   char* d = (char*)ctx->ch_ws;
   ChainBufs w;

@@ -25,6 +25,7 @@ __global__ __launch_bounds__(64) void classic_kernel(htp_classic_batch in, doubl
 
 int enqueue(htp_ctx* ctx, const htp_classic_batch& in, const htp_classic_result& out, hipStream_t s) {
   const size_t need = sizeof(double) * ct::SCR_PER_POINT * (size_t)in.cap_samples * (size_t)in.batch;
+  if (order_after(ctx, ctx->ct_ev1, s)) return -1;
   if (ensure(ctx, &ctx->ct_ws, &ctx->ct_ws_bytes, need)) return -1;
   HIPCHK(hipEventRecord(ctx->ct_ev0, s));
   hipLaunchKernelGGL(classic_kernel, dim3(in.batch), dim3(64), 0, s, in, (double*)ctx->ct_ws, out);

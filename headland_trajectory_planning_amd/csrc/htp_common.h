@@ -102,6 +102,7 @@ struct Layout {
   int64_t wx, ws, wyc, wyd, wzL, wzU, wvL, wvU, wR, wzR, wc, wd, wdx, wds, wdyc, wdyd, wdR;
   int64_t ax;                                                // last acceptable iterate (x)
   int64_t plist;                                             // compacted block indices (local sweeps, pass 2)
+  int64_t lfac;                                              // factored local blocks (LocalStore, P records)
   int64_t total;
 };
 
@@ -200,6 +201,9 @@ inline Layout make_layout(const Dims& d) {
   L.wdx = take(d.n); L.wds = take(d.md); L.wdyc = take(d.mc); L.wdyd = take(d.md); L.wdR = take(nR);
   L.ax = take(d.n);
   L.plist = take(d.P);
+  // LocalStore<MAXE, MAXE>::COUNT fields per local block (the widest kernel instance; obca_core.h)
+  constexpr int64_t LF_MAX = (2 * MAXE + 2) * (2 * MAXE + 3) / 2 + 3 * (2 * MAXE + 2) + 2 * (2 * MAXE) + 2 + 4 + 1;
+  L.lfac = take(d.form == 0 ? LF_MAX * d.P : 0);
   L.total = o;
   return L;
 }

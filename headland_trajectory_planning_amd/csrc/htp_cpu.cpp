@@ -70,3 +70,13 @@ extern "C" int htp_cpu_rs_all_paths(const double* q, int64_t cap_paths, int64_t 
   return htp::rs::all_paths_host(q, cap_paths, cap_points, n_paths, n_points, lengths, ctypes, L, point_offsets, x, y,
                                  yaw, cs, dir);
 }
+
+// The planner cores' correctly rounded libm (htp_libm.h), host build: the generator's and the tests' twin of
+// htp_libm_batch_device.
+#include "libm_batch.h"
+
+extern "C" int htp_cpu_libm_batch(int32_t fn, const double* x, const double* y, double* out, int64_t n) {
+  if (fn < 0 || fn >= htp::hm::F_COUNT || n < 0 || (n > 0 && (!x || !out))) return -1;
+  for (int64_t i = 0; i < n; ++i) out[i] = htp::hm::eval(fn, x[i], y ? y[i] : 0.0);
+  return 0;
+}

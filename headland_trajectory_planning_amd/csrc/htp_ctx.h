@@ -21,6 +21,7 @@ struct htp_ctx {
   Shape* shape = nullptr;   // device copy of the launch-uniform shape
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0.0;
+  const void* last_queue = nullptr;   // host queue of the last solve launch (queue mode), else nullptr
   // Reeds-Shepp batch (htp_rs.hip)
   void* rs_scratch = nullptr;
   size_t rs_scratch_bytes = 0;
@@ -59,6 +60,13 @@ static inline int fail(htp_ctx* c, const std::string& m) {
     hipError_t e_ = (expr);                                                          \
     if (e_ != hipSuccess) return fail(ctx, std::string(#expr ": ") + hipGetErrorString(e_)); \
   } while (0)
+
+// A launch that reuses one of the context's workspaces is ordered after the previous launch that used it
+// (`done` = that launch's end event): stream order when both are on one stream, an event wait otherwise.
+static inline int order_after(htp_ctx* ctx, hipEvent_t done, hipStream_t s) {
+  if (done && hipEventQuery(done) == hipErrorNotReady) HIPCHK(hipStreamWaitEvent(s, done, 0));
+  return 0;
+}
 
 static inline int ensure(htp_ctx* ctx, void** p, size_t* have, size_t need) {
   if (*have >= need) return 0;

@@ -274,18 +274,21 @@ bool uniform44(const Dims& D) {
 }
 
 // Shared launch path of the static-range and queue modes.
-// One launch in flight per context: the ticket counter, the per-wave workspace and the result
-// scratch belong to the context, so a second launch (any stream) before the previous one has
-// completed would share them.  Rejected loudly instead.
-int check_idle(htp_ctx* ctx) {
-  if (ctx->ev1 && hipEventQuery(ctx->ev1) == hipErrorNotReady)
-    return fail(ctx, "[OBCA] a solve launch of this context is still running (one launch in flight per htp_ctx)");
-  return 0;
+// The ticket counter, the per-wave workspace and the result scratch belong to the context: a launch is ordered
+// after the context's previous one (stream order, or an event wait across streams).  A queue-mode launch whose
+// queue is still open never ends by itself, so a launch behind it is rejected loudly instead of waiting forever.
+int check_idle(htp_ctx* ctx, hipStream_t s) {
+  if (ctx->ev1 && hipEventQuery(ctx->ev1) == hipErrorNotReady) {
+    const QueueHost* q = (const QueueHost*)ctx->last_queue;
+    if (q && !__atomic_load_n(&q->closed, __ATOMIC_ACQUIRE))
+      return fail(ctx, "[OBCA] the previous queue launch of this context is still open (htp_queue_close it first)");
+  }
+  return order_after(ctx, ctx->ev1, s);
 }
 
 int launch_solve(htp_ctx* ctx, const htp_obca_batch* in, const htp_obca_result* out, hipStream_t s, WorkSrc src,
                  int64_t waves, bool keep_results) {
-  if (check_idle(ctx)) return -1;
+  if (check_idle(ctx, s)) return -1;
   Dims D;
   make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
   Layout L = make_layout(D);
@@ -321,6 +324,7 @@ int launch_solve(htp_ctx* ctx, const htp_obca_batch* in, const htp_obca_result* 
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1, s));
+  ctx->last_queue = src.q;
   return 0;
 }
 
@@ -498,7 +502,7 @@ int htp_obca_points_solve_batch_device(htp_ctx* ctx, const htp_obca_points_batch
   if (in->batch == 0) return 0;
   if (!out->x) return fail(ctx, "[OBCA] out->x is required");
   HIPCHK(hipSetDevice(ctx->device));
-  if (check_idle(ctx)) return -1;
+  if (check_idle(ctx, (hipStream_t)stream)) return -1;
   Dims D;
   make_dims_points(D, in->N, in->M, in->n_vertices, in->obs_edges);
   Layout L = make_layout(D);
@@ -531,6 +535,7 @@ int htp_obca_points_solve_batch_device(htp_ctx* ctx, const htp_obca_points_batch
                        src, ov);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1, s));
+  ctx->last_queue = nullptr;
   return 0;
 }
 

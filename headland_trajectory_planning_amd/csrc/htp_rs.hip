@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void rs_fill(const double* __restrict__ q, int
   const int n = cnt[g];
   if (n == 0 || base + n > out.cap_points) return;
   GlobalSink gs{out.x + base, out.y + base, out.yaw + base, out.cs + base, out.directions + base, n,
-                a[0], a[1], a[2], cos(-a[2]), sin(-a[2])};
+                a[0], a[1], a[2], htp::hm::cos(-a[2]), htp::hm::sin(-a[2])};
   local_course(p, maxc, step * maxc, gs);
 }
 

@@ -136,6 +136,22 @@ struct LocalBlock {
   }
 };
 
+// Factored local blocks kept for the KKT solves (HTP_STORE_LOCAL): the factor sweep stores every unpivoted
+// block's LDL^T factor and the rows the solves read, structure-of-arrays (field f of block p at f * P + p, so a
+// wave's 64 blocks load as one coalesced 512-byte access per field); the right-hand-side and back sweeps of every
+// KKT solve with that factorization (the step, its second-order corrections) load them instead of rebuilding
+// and refactoring each block.  The same doubles either way.
+#ifndef HTP_STORE_LOCAL
+#define HTP_STORE_LOCAL 1
+#endif
+template <int EN, int EM>
+struct LocalStore {
+  static constexpr int NZ = EN + EM, NL = NZ + 2, NPK = NL * (NL + 1) / 2;
+  static constexpr int F_K = 0, F_B = NPK, F_J1 = F_B + 3 * NL, F_J3Z = F_J1 + NZ, F_J3P = F_J3Z + NZ;
+  static constexpr int F_E1 = F_J3P + 2, F_E3 = F_E1 + 1, F_DS1 = F_E3 + 1, F_DS3 = F_DS1 + 1, F_PIV = F_DS3 + 1;
+  static constexpr int COUNT = F_PIV + 1;
+};
+
 // ---------------------------------------------------------------------------
 // Point-formulation local block (R/obca_py/optimizer_points.py:282-327):
 // z = lam_ji (EM) of obstacle j at step i, no equality rows; its 2 KV
@@ -1200,6 +1216,51 @@ struct ObcaSolver {
     for (int k = 0; k < nrhs; ++k) bk_solve_packed(B.K, ip, NL, V + k * NL);
   }
 
+  // LocalStore record of block p (HTP_STORE_LOCAL): written by the factor sweep, read by the solve sweeps
+  template <int EN, int EM>
+  HTP_HD HTP_FI void store_local(const LocalBlock<EN, EM>& B, int p, bool piv) {
+    using S = LocalStore<EN, EM>;
+    gd* F = A(L.lfac) + p;
+    const int64_t P = D.P;
+    F[S::F_PIV * P] = piv ? 1.0 : 0.0;
+    if (piv) return;
+    for (int q = 0; q < S::NPK; ++q) F[(S::F_K + q) * P] = B.K[q];
+    for (int r = 0; r < S::NL; ++r)
+      for (int col = 0; col < 3; ++col) F[(S::F_B + 3 * r + col) * P] = B.B[r][col];
+    for (int j = 0; j < S::NZ; ++j) {
+      F[(S::F_J1 + j) * P] = B.J1[j];
+      F[(S::F_J3Z + j) * P] = B.J3z[j];
+    }
+    F[S::F_J3P * P] = B.J3p[0];
+    F[(S::F_J3P + 1) * P] = B.J3p[1];
+    F[S::F_E1 * P] = B.E1;
+    F[S::F_E3 * P] = B.E3;
+    F[S::F_DS1 * P] = B.Ds1;
+    F[S::F_DS3 * P] = B.Ds3;
+  }
+  // true: block p took the pivoted path (its record holds only the flag)
+  template <int EN, int EM>
+  HTP_HD HTP_FI bool load_local(LocalBlock<EN, EM>& B, int p) const {
+    using S = LocalStore<EN, EM>;
+    const gd* F = A(L.lfac) + p;
+    const int64_t P = D.P;
+    if (F[S::F_PIV * P] != 0.0) return true;
+    for (int q = 0; q < S::NPK; ++q) B.K[q] = F[(S::F_K + q) * P];
+    for (int r = 0; r < S::NL; ++r)
+      for (int col = 0; col < 3; ++col) B.B[r][col] = F[(S::F_B + 3 * r + col) * P];
+    for (int j = 0; j < S::NZ; ++j) {
+      B.J1[j] = F[(S::F_J1 + j) * P];
+      B.J3z[j] = F[(S::F_J3Z + j) * P];
+    }
+    B.J3p[0] = F[S::F_J3P * P];
+    B.J3p[1] = F[(S::F_J3P + 1) * P];
+    B.E1 = F[S::F_E1 * P];
+    B.E3 = F[S::F_E3 * P];
+    B.Ds1 = F[S::F_DS1 * P];
+    B.Ds3 = F[S::F_DS3 * P];
+    return false;
+  }
+
   // The three local sweeps run in two passes.  Pass 1: lane-parallel over the blocks; a block whose
   // unpivoted LDL^T meets a non-positive multiplier pivot (B.piv: ~11 % of the blocks of config D)
   // is only recorded, its index compacted into L.plist (ballot rank).  Pass 2: the recorded blocks,
@@ -1227,6 +1288,9 @@ struct ObcaSolver {
         build_local<EN, EM>(B, p, ls, dw, dc);
         B.factor();
         piv = B.piv;
+#if HTP_STORE_LOCAL
+        store_local<EN, EM>(B, p, piv);
+#endif
         if (!piv) {
           neg += B.neg;
           zero |= B.zero;
@@ -1322,9 +1386,13 @@ struct ObcaSolver {
       bool piv = false;
       if (p < D.P) {
         LocalBlock<EN, EM> B;
+#if HTP_STORE_LOCAL
+        piv = load_local<EN, EM>(B, p);
+#else
         build_local<EN, EM>(B, p, ls, dw, dc);
         B.factor();
         piv = B.piv;
+#endif
         if (!piv) {
           double v[NL], q3;
           rhs(p, B, v, q3);
@@ -1414,9 +1482,13 @@ struct ObcaSolver {
       bool piv = false;
       if (p < D.P) {
         LocalBlock<EN, EM> B;
+#if HTP_STORE_LOCAL
+        piv = load_local<EN, EM>(B, p);
+#else
         build_local<EN, EM>(B, p, ls, dw, dc);
         B.factor();
         piv = B.piv;
+#endif
         if (!piv) {
           double v[NL], dpx, dpy;
           rhs(p, B, v, dpx, dpy);

@@ -26,6 +26,8 @@
 #error "define HTP_HD before including oge_core.h"
 #endif
 
+#include "htp_libm.h"
+
 namespace htp {
 namespace oge {
 
@@ -91,7 +93,7 @@ struct Scene {
 // create_tree_rows(row_num, row_width, row_lengths, slope_angle, l_std) with the given draws
 HTP_HD inline void make_rows(const SceneIn& in, Scene& S) {
   S.n = in.nrows;
-  const double dx = in.row_width * tan(in.slope);
+  const double dx = in.row_width * hm::tan(in.slope);
   for (int i = 0; i < S.n; ++i) {
     const double y = in.row_width * i;
     double x = dx * i;
@@ -114,7 +116,7 @@ HTP_HD inline double headland_angle(const Scene& S, int side) {
   if (pstd(xs, S.n) < 0.01) return 3.141592653589793 / 2;
   double k, b;
   polyfit1(xs, ys, S.n, k, b);
-  return atan(k);
+  return hm::atan(k);
 }
 
 // get_map_exterior_pts(headland_width) :288-334 -> 2 n points (near rows, then far rows reversed)
@@ -124,7 +126,7 @@ HTP_HD inline int exterior_pts(const Scene& S, double hw, double (*P)[2]) {
   for (int i = 1; i < n; ++i) acc += S.ry[i][0] - S.ry[i - 1][0];
   const double rw = acc / (n - 1);
   const double na = headland_angle(S, NEAR), fa = headland_angle(S, FAR);
-  const double dxn = fabs(hw / sin(na)), dxf = fabs(hw / sin(fa));
+  const double dxn = fabs(hw / hm::sin(na)), dxf = fabs(hw / hm::sin(fa));
   int up = 0, lo = 0;
   for (int i = 0; i < n; ++i) {
     P[i][0] = S.rx[i][0] - dxn;
@@ -132,7 +134,7 @@ HTP_HD inline int exterior_pts(const Scene& S, double hw, double (*P)[2]) {
   }
   for (int i = 1; i < n; ++i) if (P[i][1] > P[up][1]) up = i;
   P[up][1] += rw;
-  double d = fabs(sin(na)) < 1e-5 ? 0.0 : rw / tan(na);
+  double d = fabs(hm::sin(na)) < 1e-5 ? 0.0 : rw / hm::tan(na);
   P[up][0] += d;
   for (int i = 1; i < n; ++i) if (P[i][1] < P[lo][1]) lo = i;
   P[lo][1] -= rw;
@@ -144,7 +146,7 @@ HTP_HD inline int exterior_pts(const Scene& S, double hw, double (*P)[2]) {
   }
   up = 0;
   lo = 0;
-  d = fabs(sin(fa)) < 1e-5 ? 0.0 : rw / tan(fa);
+  d = fabs(hm::sin(fa)) < 1e-5 ? 0.0 : rw / hm::tan(fa);
   for (int i = 1; i < n; ++i) if (F[i][1] > F[up][1]) up = i;
   F[up][1] += rw;
   F[up][0] += d;

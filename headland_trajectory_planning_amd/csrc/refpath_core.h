@@ -15,6 +15,7 @@
 //     v = 0 at both ends (:108-111).
 #pragma once
 #include <cmath>
+#include "htp_libm.h"
 #include <cstdint>
 
 #include "dubins_core.h"
@@ -72,7 +73,7 @@ struct Course {
       return -1;
     }
     S[0] = 0.0;
-    for (int i = 1; i < m; ++i) S[i] = S[i - 1] + hypot(X[i] - X[i - 1], Y[i] - Y[i - 1]);
+    for (int i = 1; i < m; ++i) S[i] = S[i - 1] + hm::hypot(X[i] - X[i - 1], Y[i] - Y[i - 1]);
     c.sync();
     if (c.lane == 0 || C::width == 1) dub::spline_slopes(S, X, m, DX, WK);
     if (c.lane == (C::width > 1 ? 1 : 0)) dub::spline_slopes(S, Y, m, DY, WK + 4 * cap);
@@ -95,10 +96,10 @@ struct Course {
       double x, x1, x2, y, y1, y2;
       dub::eval3(S, X, DX, iv, v, x, x1, x2);
       dub::eval3(S, Y, DY, iv, v, y, y1, y2);
-      double yaw = atan2(y1, x1);
-      const double kap = (y2 * x1 - x2 * y1) / pow(x1 * x1 + y1 * y1, 1.5);
+      double yaw = hm::atan2(y1, x1);
+      const double kap = (y2 * x1 - x2 * y1) / hm::pow(x1 * x1 + y1 * y1, 1.5);
       if (rev) yaw = wrap_angle(yaw + PI);
-      double steer = atan(wb * kap) * (rev ? -1.0 : 1.0);
+      double steer = hm::atan(wb * kap) * (rev ? -1.0 : 1.0);
       double vel = 1.0 * gear * desired_v;
       if (k == 0) {
         vel = 0.0;

@@ -24,6 +24,8 @@
 #error "define HTP_HD before including rs_core.h"
 #endif
 
+#include "htp_libm.h"
+
 namespace htp {
 namespace rs {
 
@@ -145,26 +147,26 @@ HTP_HD inline void add_path(PathSet& S, int n, const double* l, const int8_t* ty
 HTP_HD inline bool w_SLS(double x, double y, double phi, double& t, double& u, double& v) {
   phi = Mreg(phi);
   if (y > 0.0 && 0.0 < phi && phi < PI * 0.99) {
-    const double xd = -y / tan(phi) + x;
-    t = xd - tan(phi / 2.0);
+    const double xd = -y / hm::tan(phi) + x;
+    t = xd - hm::tan(phi / 2.0);
     u = phi;
-    v = sqrt(pow(x - xd, 2.0) + pow(y, 2.0)) - tan(phi / 2.0);
+    v = sqrt(hm::pow(x - xd, 2.0) + hm::pow(y, 2.0)) - hm::tan(phi / 2.0);
     return true;
   }
   if (y < 0.0 && 0.0 < phi && phi < PI * 0.99) {
-    const double xd = -y / tan(phi) + x;
-    t = xd - tan(phi / 2.0);
+    const double xd = -y / hm::tan(phi) + x;
+    t = xd - hm::tan(phi / 2.0);
     u = phi;
-    v = -sqrt(pow(x - xd, 2.0) + pow(y, 2.0)) - tan(phi / 2.0);
+    v = -sqrt(hm::pow(x - xd, 2.0) + hm::pow(y, 2.0)) - hm::tan(phi / 2.0);
     return true;
   }
   return false;
 }
 
 HTP_HD inline bool w_LSL(double x, double y, double phi, double& t, double& u, double& v) {
-  const double a = x - sin(phi), b = y - 1.0 + cos(phi);
+  const double a = x - hm::sin(phi), b = y - 1.0 + hm::cos(phi);
   u = py_hypot(a, b);
-  t = atan2(b, a);
+  t = hm::atan2(b, a);
   if (t >= 0.0) {
     v = Mreg(phi - t);
     if (v >= 0.0) return true;
@@ -173,13 +175,13 @@ HTP_HD inline bool w_LSL(double x, double y, double phi, double& t, double& u, d
 }
 
 HTP_HD inline bool w_LSR(double x, double y, double phi, double& t, double& u, double& v) {
-  const double a = x + sin(phi), b = y - 1.0 - cos(phi);
+  const double a = x + hm::sin(phi), b = y - 1.0 - hm::cos(phi);
   double u1 = py_hypot(a, b);
-  const double t1 = atan2(b, a);
-  u1 = pow(u1, 2.0);  // Python u1**2 (libm pow on the host harness)
+  const double t1 = hm::atan2(b, a);
+  u1 = hm::pow(u1, 2.0);  // Python u1**2 (libm pow on the host harness)
   if (u1 >= 4.0) {
     u = sqrt(u1 - 4.0);
-    const double theta = atan2(2.0, u);
+    const double theta = hm::atan2(2.0, u);
     t = Mreg(t1 + theta);
     v = Mreg(t - phi);
     if (t >= 0.0 && v >= 0.0) return true;
@@ -188,11 +190,11 @@ HTP_HD inline bool w_LSR(double x, double y, double phi, double& t, double& u, d
 }
 
 HTP_HD inline bool w_LRL(double x, double y, double phi, double& t, double& u, double& v) {
-  const double a = x - sin(phi), b = y - 1.0 + cos(phi);
+  const double a = x - hm::sin(phi), b = y - 1.0 + hm::cos(phi);
   const double u1 = py_hypot(a, b);
-  const double t1 = atan2(b, a);
+  const double t1 = hm::atan2(b, a);
   if (u1 <= 4.0) {
-    u = -2.0 * asin(0.25 * u1);
+    u = -2.0 * hm::asin(0.25 * u1);
     t = Mreg(t1 + 0.5 * u + PI);
     v = Mreg(phi - t + u);
     if (t >= 0.0 && u <= 0.0) return true;
@@ -202,19 +204,19 @@ HTP_HD inline bool w_LRL(double x, double y, double phi, double& t, double& u, d
 
 HTP_HD inline void tau_omega(double u, double v, double xi, double eta, double phi, double& tau, double& omega) {
   const double delta = Mreg(u - v);
-  const double A = sin(u) - sin(delta);
-  const double B = cos(u) - cos(delta) - 1.0;
-  const double t1 = atan2(eta * A - xi * B, xi * A + eta * B);
-  const double t2 = 2.0 * (cos(delta) - cos(v) - cos(u)) + 3.0;
+  const double A = hm::sin(u) - hm::sin(delta);
+  const double B = hm::cos(u) - hm::cos(delta) - 1.0;
+  const double t1 = hm::atan2(eta * A - xi * B, xi * A + eta * B);
+  const double t2 = 2.0 * (hm::cos(delta) - hm::cos(v) - hm::cos(u)) + 3.0;
   tau = (t2 < 0) ? Mreg(t1 + PI) : Mreg(t1);
   omega = Mreg(tau - u + v - phi);
 }
 
 HTP_HD inline bool w_LRLRn(double x, double y, double phi, double& t, double& u, double& v) {
-  const double xi = x + sin(phi), eta = y - 1.0 - cos(phi);
+  const double xi = x + hm::sin(phi), eta = y - 1.0 - hm::cos(phi);
   const double rho = 0.25 * (2.0 + sqrt(xi * xi + eta * eta));
   if (rho <= 1.0) {
-    u = acos(rho);
+    u = hm::acos(rho);
     tau_omega(u, -u, xi, eta, phi, t, v);
     if (t >= 0.0 && v <= 0.0) return true;
   }
@@ -222,10 +224,10 @@ HTP_HD inline bool w_LRLRn(double x, double y, double phi, double& t, double& u,
 }
 
 HTP_HD inline bool w_LRLRp(double x, double y, double phi, double& t, double& u, double& v) {
-  const double xi = x + sin(phi), eta = y - 1.0 - cos(phi);
+  const double xi = x + hm::sin(phi), eta = y - 1.0 - hm::cos(phi);
   const double rho = (20.0 - xi * xi - eta * eta) / 16.0;
   if (0.0 <= rho && rho <= 1.0) {
-    u = -acos(rho);
+    u = -hm::acos(rho);
     if (u >= -0.5 * PI) {
       tau_omega(u, u, xi, eta, phi, t, v);
       if (t >= 0.0 && v >= 0.0) return true;
@@ -235,8 +237,8 @@ HTP_HD inline bool w_LRLRp(double x, double y, double phi, double& t, double& u,
 }
 
 HTP_HD inline bool w_LRSR(double x, double y, double phi, double& t, double& u, double& v) {
-  const double xi = x + sin(phi), eta = y - 1.0 - cos(phi);
-  const double rho = py_hypot(-eta, xi), theta = atan2(xi, -eta);
+  const double xi = x + hm::sin(phi), eta = y - 1.0 - hm::cos(phi);
+  const double rho = py_hypot(-eta, xi), theta = hm::atan2(xi, -eta);
   if (rho >= 2.0) {
     t = theta;
     u = 2.0 - rho;
@@ -247,12 +249,12 @@ HTP_HD inline bool w_LRSR(double x, double y, double phi, double& t, double& u, 
 }
 
 HTP_HD inline bool w_LRSL(double x, double y, double phi, double& t, double& u, double& v) {
-  const double xi = x - sin(phi), eta = y - 1.0 + cos(phi);
-  const double rho = py_hypot(xi, eta), theta = atan2(eta, xi);
+  const double xi = x - hm::sin(phi), eta = y - 1.0 + hm::cos(phi);
+  const double rho = py_hypot(xi, eta), theta = hm::atan2(eta, xi);
   if (rho >= 2.0) {
     const double r = sqrt(rho * rho - 4.0);
     u = 2.0 - r;
-    t = Mreg(theta + atan2(r, -2.0));
+    t = Mreg(theta + hm::atan2(r, -2.0));
     v = Mreg(phi - 0.5 * PI - t);
     if (t >= 0.0 && u <= 0.0 && v <= 0.0) return true;
   }
@@ -260,12 +262,12 @@ HTP_HD inline bool w_LRSL(double x, double y, double phi, double& t, double& u, 
 }
 
 HTP_HD inline bool w_LRSLR(double x, double y, double phi, double& t, double& u, double& v) {
-  const double xi = x + sin(phi), eta = y - 1.0 - cos(phi);
+  const double xi = x + hm::sin(phi), eta = y - 1.0 - hm::cos(phi);
   const double rho = py_hypot(xi, eta);
   if (rho >= 2.0) {
     u = 4.0 - sqrt(rho * rho - 4.0);
     if (u <= 0.0) {
-      t = Mreg(atan2((4.0 - u) * xi - 2.0 * eta, -2.0 * xi + (u - 4.0) * eta));
+      t = Mreg(hm::atan2((4.0 - u) * xi - 2.0 * eta, -2.0 * xi + (u - 4.0) * eta));
       v = Mreg(t - phi);
       if (t >= 0.0 && v >= 0.0) return true;
     }
@@ -360,11 +362,11 @@ HTP_HD inline void generate_paths(double sx, double sy, double syaw, double gx, 
   S.n = 0;
   S.err = 0;
   const double dx = gx - sx, dy = gy - sy, dth = gyaw - syaw;
-  const double c = cos(syaw), s = sin(syaw);
+  const double c = hm::cos(syaw), s = hm::sin(syaw);
   const double x = (c * dx + s * dy) * maxc;
   const double y = (-s * dx + c * dy) * maxc;
-  const double xb = x * cos(dth) + y * sin(dth);
-  const double yb = x * sin(dth) - y * cos(dth);
+  const double xb = x * hm::cos(dth) + y * hm::sin(dth);
+  const double yb = x * hm::sin(dth) - y * hm::cos(dth);
   const Cand* T = cand_table();
   for (int k = 0; k < 46; ++k) {
     const Cand& cd = T[k];
@@ -386,17 +388,17 @@ HTP_HD inline void generate_paths(double sx, double sy, double syaw, double gx, 
 HTP_HD inline void interp(double l, int m, double maxc, double ox, double oy, double oyaw, double& px, double& py,
                           double& pyaw, double& cs, int& dir) {
   if (m == SEG_S) {
-    px = ox + l / maxc * cos(oyaw);
-    py = oy + l / maxc * sin(oyaw);
+    px = ox + l / maxc * hm::cos(oyaw);
+    py = oy + l / maxc * hm::sin(oyaw);
     pyaw = oyaw;
     cs = 0.0;
   } else {
-    const double ldx = sin(l) / maxc;
+    const double ldx = hm::sin(l) / maxc;
     double ldy;
-    if (m == SEG_L) { ldy = (1.0 - cos(l)) / maxc; cs = maxc; }
-    else { ldy = (1.0 - cos(l)) / (-maxc); cs = -maxc; }
-    const double gdx = cos(-oyaw) * ldx + sin(-oyaw) * ldy;
-    const double gdy = -sin(-oyaw) * ldx + cos(-oyaw) * ldy;
+    if (m == SEG_L) { ldy = (1.0 - hm::cos(l)) / maxc; cs = maxc; }
+    else { ldy = (1.0 - hm::cos(l)) / (-maxc); cs = -maxc; }
+    const double gdx = hm::cos(-oyaw) * ldx + hm::sin(-oyaw) * ldy;
+    const double gdy = -hm::sin(-oyaw) * ldx + hm::cos(-oyaw) * ldy;
     px = ox + gdx;
     py = oy + gdy;
   }

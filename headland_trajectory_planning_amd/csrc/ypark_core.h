@@ -13,6 +13,7 @@
 // reference's answer; later chunks are never built.
 #pragma once
 #include <cmath>
+#include "htp_libm.h"
 #include <cstdint>
 
 #include "hastar_core.h"
@@ -39,20 +40,20 @@ enum { ST_FOUND = 0, ST_NONE = 1, ST_END_BLOCKED = 2, ST_BAD_INPUT = 3 };
 HTP_HD inline int motion_path(double x0, double y0, double yaw0, double steer, double dir, double length,
                               double wb, double step, double* P) {
   const int n = (int)rint(length / step);
-  const double yaw_step = dir * step / wb * tan(steer);
+  const double yaw_step = dir * step / wb * hm::tan(steer);
   const double init_yaw = ha::angle_wrap(yaw0 + yaw_step);
   const double stop = init_yaw + yaw_step * (double)n;
   const double div = (double)n;
   const double delta = stop - init_yaw;
   const double stp = delta / div;
-  const double curv = fabs(steer) > 0.00001 ? tan(steer) / wb : 0.0;
+  const double curv = fabs(steer) > 0.00001 ? hm::tan(steer) / wb : 0.0;
   P[0] = x0; P[1] = y0; P[2] = yaw0; P[3] = curv; P[4] = dir;
   double ax = 0.0, ay = 0.0;
   for (int i = 0; i < n; ++i) {  // xs from yaws[:-1], path yaw = yaws[1:]
     const double yi = (stp == 0) ? ((double)i / div) * delta + init_yaw : (double)i * stp + init_yaw;
     const double wy = ha::angle_wrap(yi);
-    const double dx = step * cos(wy) * dir;
-    const double dy = step * sin(wy) * dir;
+    const double dx = step * hm::cos(wy) * dir;
+    const double dy = step * hm::sin(wy) * dir;
     ax = (i == 0) ? dx : ax + dx;
     ay = (i == 0) ? dy : ay + dy;
     const double ni = (i + 1 == n) ? stop

@@ -658,11 +658,12 @@ def make_orchard_instance(pid, N=80, M=6, implement="none", key=20251015, turn="
         ds = Lp / (N - 1)
         desired_v = min(ds / dT, 0.9)
         try:
-            # spline spacing just above half the resampled spacing: Lp / (2 N - 1.5), not Lp / (2 N - 2), so the
-            # sample count ceil((S + ds) / ds) of a single-gear turn (S = Lp) is not an exact integer boundary that
-            # one rounding ulp (host vs device libm) would decide
+            # spline spacing half the resampled spacing, Lp / (2 N - 2): a single-gear turn's sample count
+            # len(np.arange(0, S + ds, ds)) then sits on an exact integer tie (S = Lp up to summation order), which
+            # the last bit of the libm decides -- the device and host builds share one correctly rounded libm
+            # (csrc/htp_libm.h), so they decide it alike (tests/test_gpu_e2e.py)
             ref = get_init_ref_path(car, path[:, 0], path[:, 1], path[:, 2], path[:, 3], path[:, 4],
-                                    desired_v=desired_v, ds=Lp / (2.0 * N - 1.5))
+                                    desired_v=desired_v, ds=Lp / (2.0 * N - 2.0))
         except ValueError:
             continue
         traj = _resample_rows(ref, N)

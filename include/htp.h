@@ -440,8 +440,8 @@ double htp_classic_last_ms(htp_ctx* ctx);
 
 /* ---------------------------------------------------------------------------
  * Orchard workload chain on the device (synth.make_orchard_instance's steps after the scene draws): for each
- * problem, the classic turn (htp_classic_turn_batch) -> get_init_ref_path at ds = L / (N - 1) / 2,
- * desired_v = min(ds / dT, 0.9) (R/obca_py/util.py:62-113) -> the init guess resampled to N rows and the
+ * problem, the classic turn (htp_classic_turn_batch) -> get_init_ref_path at spacing ds / 2 = L / (2N - 2)
+ * (ds = L / (N - 1), the resampled spacing), desired_v = min(ds / dT, 0.9) (R/obca_py/util.py:62-113) -> the init guess resampled to N rows and the
  * headland width the warm start needs -> the OGE_OBCA obstacle producer (htp_oge_obstacles_batch) -> quads,
  * the M nearest, halfspaces.  Writes the htp_obca_batch arrays traj / obs_A / obs_b (4 edges per obstacle)
  * in HBM, enqueued on `stream`; intermediates live in the context.  `scenes` and `turns` hold device
@@ -464,6 +464,18 @@ typedef struct {
 } htp_chain_batch;
 int htp_orchard_chain_device(htp_ctx* ctx, const htp_chain_batch* in, void* stream);
 double htp_chain_last_ms(htp_ctx* ctx);
+
+
+/* ---- correctly rounded libm of the planner cores (csrc/htp_libm.h) ----------------------------------------
+ * Replaces nothing in the reference: the reference's planners call CPython's math module / numpy (glibc, or
+ * numpy's SIMD kernels), whose last bits differ between platforms.  Every device planner kernel and every host
+ * build of the same cores evaluates sin, cos, tan, atan, atan2, asin, acos, hypot and pow with this one
+ * correctly rounded implementation, so integer outputs that hang on the last bit (a spline piece's sample
+ * count, R/path_planner/utils/cubic_spline.py:102) are identical on the GPU and on the host.
+ * fn: 0 sin, 1 cos, 2 tan, 3 atan, 4 atan2(x[i], y[i]), 5 asin, 6 acos, 7 hypot(x[i], y[i]), 8 pow(x[i], y[i]).
+ * x, y, out: device arrays of n doubles (y only for the two-argument functions). */
+int htp_libm_batch_device(htp_ctx* ctx, int32_t fn, const double* x, const double* y, double* out, int64_t n,
+                          void* stream);
 
 #ifdef __cplusplus
 }

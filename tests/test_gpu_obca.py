@@ -146,32 +146,34 @@ def _stationarity(nlp, x, tol_act=1e-3):
 
 
 # Problems of the first 64 of a config that the host build of the solver core does not solve (max_cpu_time
-# off, profiles/r03h_screen_*.json); each is pinned by an oracle fixture (tests/golden/obca_full A43, C36:
-# Infeasible_Problem_Detected in both), so the GPU must fail exactly these, with that status.  (C59, failing in an
-# earlier version of the generator that could list a tree row twice, keeps its fixture with its own instance.)
+# off, profiles/r04_screen_{A,B,C}.json); each is pinned by an oracle fixture made from the same instance
+# (tests/golden/obca_full A43, C36: Infeasible_Problem_Detected in both), so the GPU must fail exactly these, with
+# that status.  (C59, failing in an earlier version of the generator that could list a tree row twice, keeps its
+# fixture with its own instance.)
 PINNED_FAILURES = {"A": {43: 7}, "B": {}, "C": {36: 7}}
+# Config E (N=160, 12 obstacles, pruner; restoration-heavy): the host build of the same core solves 14 of the
+# first 16 and stops E4 and E12 at the 3000-iteration limit after 106 / 135 restoration phases
+# (profiles/r04_screen_E16.json).  With max_cpu_time off (a wall-clock limit would make the outcome depend on
+# GPU load) the device must solve at least those 14.
+E_MIN_OK = 14 / 16
 
 
-@pytest.mark.parametrize("cfg,nprob,min_ok", [("A", 64, None), ("B", 64, None), ("C", 64, None), ("E", 16, 0.75)])
+@pytest.mark.parametrize("cfg,nprob,min_ok", [("A", 64, None), ("B", 64, None), ("C", 64, None), ("E", 16, E_MIN_OK)])
 def test_full_config_properties(ctx, cfg, nprob, min_ok):
-    """Configs at their turn types and scenes (synth.config_instance: the reference's producers)."""
+    """Configs at their turn types and scenes (synth.config_instance: the reference's producers), max_cpu_time
+    off so that every status is deterministic."""
     insts = [synth.config_instance(cfg, pid) for pid in range(nprob)]
     pk = _native.PackedBatch(insts)
-    # config E (N=160, 12 obstacles, pruner) is restoration-heavy (E3: 356 iterations / 30 restoration phases
-    # in the oracle too); it runs under the reference's default max_cpu_time (optimizer.py:475)
-    ctx.set_option("max_cpu_time", 20.0 if cfg == "E" else 0.0)
-    try:
-        res = ctx.solve(pk)
-        solo = ctx.solve(_native.PackedBatch([insts[5]]))
-        again = ctx.solve(pk)
-    finally:
-        ctx.set_option("max_cpu_time", 0.0)
+    ctx.set_option("max_cpu_time", 0.0)
+    res = ctx.solve(pk)
+    solo = ctx.solve(_native.PackedBatch([insts[5]]))
+    again = ctx.solve(pk)
     ok = np.isin(res.status, [0, 1])
     if cfg in PINNED_FAILURES:
         fails = {int(k): int(res.status[k]) for k in np.where(~ok)[0]}
         assert fails == PINNED_FAILURES[cfg], fails
     else:
-        assert ok.mean() >= min_ok, np.bincount(res.status)
+        assert ok.mean() >= min_ok, (np.bincount(res.status), np.where(~ok)[0], res.iterations[~ok])
     for k in np.where(ok)[0][:6]:
         nlp = ObcaNLP(insts[k])
         cv, bv = _kkt_residuals(nlp, res.x[k])
@@ -180,11 +182,9 @@ def test_full_config_properties(ctx, cfg, nprob, min_ok):
             assert _stationarity(nlp, res.x[k]) <= 1e-5, k
     # batch-composition invariance: problem 5 alone == problem 5 inside the batch
     assert np.array_equal(solo.x[0], res.x[5])
-    # determinism (problems stopped by the wall-clock limit in either run excepted: the limit may fall in
-    # different iterations of two runs)
-    det = (res.status != 6) & (again.status != 6)
-    assert np.array_equal(again.status[det], res.status[det])
-    assert np.array_equal(again.x[det], res.x[det])
+    # determinism
+    assert np.array_equal(again.status, res.status)
+    assert np.array_equal(again.x, res.x)
 
 
 def test_max_cpu_time_stops_the_solve(ctx):

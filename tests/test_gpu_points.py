@@ -34,8 +34,8 @@ def _feasible(inst, x, tol=1e-6):
 
 def test_gpu_matches_oracle_quads(ctx):
     """24 small problems against the oracle (ground truth): same status; without a restoration phase
-    the same iteration count (+-1) and states within 1e-6; through restoration the paths may settle on
-    distinct local minima of this nonconvex NLP (both feasible)."""
+    the same iteration count (+-1) and states within 1e-6; through restoration (optimizer_points.py:157-191
+    hands IPOPT the same NLP) states within the north_star tolerance 1e-4 and a feasible point."""
     insts = [synth.make_points_instance(pid, N=12, M=2) for pid in range(24)]
     g = ctx.solve_points(_native.PointsPackedBatch(insts))
     bad = []
@@ -46,7 +46,7 @@ def test_gpu_matches_oracle_quads(ctx):
         if ok and ref["n_resto"] == 0 and g.n_resto[k] == 0:
             ok = abs(int(g.iterations[k]) - ref["iters"]) <= 1 and err < 1e-6
         elif ok and g.status[k] in (0, 1):
-            ok = _feasible(inst, g.x[k])
+            ok = err <= 1e-4 and _feasible(inst, g.x[k])
         if not ok:
             bad.append((k, int(g.status[k]), int(g.iterations[k]), int(g.n_resto[k]), ref["status"], ref["iters"],
                         ref["n_resto"], err))

@@ -4,7 +4,8 @@
   repeats: every ticket's status / iterations / objective / restorations and every x row equal, bit
   for bit, the static-range solve of the same problems (same kernel, one wave per problem);
 * closing early: tickets that were never published stay unwritten and the launch drains;
-* one launch in flight per context: a second launch while the first runs is rejected."""
+* launches of one context are ordered: a second launch (any stream) waits for the first; only a launch behind
+  a queue launch whose queue is still open is rejected (it would wait forever)."""
 import time
 
 import numpy as np
@@ -49,7 +50,7 @@ def test_queue_tickets_published_after_launch_match_static_solve():
     stream = torch.cuda.Stream(dev)
     try:
         ctx.solve_queue_device(pk, ptrs, q, optr, stream=stream.cuda_stream, waves=4, max_wait_s=30.0)
-        with pytest.raises(RuntimeError, match="still running"):   # one launch in flight per context
+        with pytest.raises(RuntimeError, match="still open"):   # behind an open queue launch: rejected
             ctx.solve_queue_device(pk, ptrs, q, optr, stream=stream.cuda_stream, waves=4, max_wait_s=30.0)
         time.sleep(0.2)
         q.publish(order1)
@@ -92,3 +93,20 @@ def test_queue_closed_early_leaves_unpublished_tickets_unwritten():
     res = ctx.solve(pk)
     assert np.array_equal(res.status[[4, 1, 2]], st[:3])
     q.destroy()
+
+
+def test_back_to_back_launches_on_two_streams_are_ordered():
+    """Two static-range launches enqueued at once on two streams share the context's workspace: the second
+    is ordered after the first (event wait), and both return the host-API solve's results."""
+    torch, pk, dev, dev_in, ptrs = _setup(8)
+    ctx = _native.Context(0)
+    ref = ctx.solve(pk)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    o1, x1, p1 = _outs(torch, dev, pk.batch, pk.n_var, pk.batch)
+    o2, x2, p2 = _outs(torch, dev, pk.batch, pk.n_var, pk.batch)
+    ctx.solve_device(pk, ptrs, p1, stream=s1.cuda_stream)
+    ctx.solve_device(pk, ptrs, p2, stream=s2.cuda_stream)
+    torch.cuda.synchronize(dev)
+    for o, x in ((o1, x1), (o2, x2)):
+        assert np.array_equal(o["status"].cpu().numpy(), ref.status)
+        assert np.array_equal(x.cpu().numpy(), ref.x)

@@ -1,0 +1,79 @@
+"""The planner cores' correctly rounded libm (csrc/htp_libm.h), host build (libhtp_cpu.so): every function
+returns the correctly rounded double (mpmath at 300 bits) on random arguments over the cores' ranges and over
+wide magnitudes (Payne-Hanek reduction for the trig functions beyond 2^20), and C99's special values.  The
+device build must return the same doubles (tests/test_gpu_libm.py); tools/libm_check.py compares 10^7
+arguments per function with glibc and numpy (profiles/r04_libm_check.json)."""
+import math
+
+import mpmath
+import numpy as np
+import pytest
+
+from headland_trajectory_planning_amd import _native
+
+MP = {"sin": mpmath.sin, "cos": mpmath.cos, "tan": mpmath.tan, "atan": mpmath.atan, "atan2": mpmath.atan2,
+      "asin": mpmath.asin, "acos": mpmath.acos, "hypot": lambda a, b: mpmath.sqrt(a * a + b * b),
+      "pow": lambda a, b: a ** b}
+
+
+def _args(name, rng, n):
+    lg = lambda a, b: np.exp(rng.uniform(np.log(a), np.log(b), n)) * rng.choice([-1.0, 1.0], n)  # noqa: E731
+    if name in ("sin", "cos", "tan"):
+        return np.concatenate([rng.uniform(-20, 20, n), lg(1e-9, 1e300)]), None
+    if name == "atan":
+        return np.concatenate([rng.uniform(-5, 5, n), lg(1e-300, 1e300)]), None
+    if name in ("asin", "acos"):
+        return np.concatenate([rng.uniform(-1, 1, n), lg(1e-20, 1)]), None
+    if name in ("atan2", "hypot"):
+        return (np.concatenate([rng.uniform(-10, 10, n), lg(1e-150, 1e150)]),
+                np.concatenate([rng.uniform(-10, 10, n), lg(1e-150, 1e150)]))
+    x = np.abs(np.concatenate([rng.uniform(0, 100, n), lg(1e-100, 1e100), rng.uniform(0.1, 10, n)]))
+    return x, np.concatenate([np.full(n, 1.5), np.full(n, 2.0), rng.uniform(-20, 20, n)])
+
+
+@pytest.mark.parametrize("name", list(_native.LIBM_FN))
+def test_correctly_rounded(name):
+    mpmath.mp.prec = 300
+    rng = np.random.default_rng(7 + _native.LIBM_FN[name])
+    x, y = _args(name, rng, 1500)
+    got = _native.cpu_libm(name, x, y)
+    for k in range(len(x)):
+        if y is None:
+            ref = float(MP[name](mpmath.mpf(float(x[k]))))
+        else:
+            ref = float(MP[name](mpmath.mpf(float(x[k])), mpmath.mpf(float(y[k]))))
+        assert got[k] == ref, (name, repr(x[k]), None if y is None else repr(y[k]), repr(got[k]), repr(ref))
+
+
+def _same(a, b):
+    return (a != a and b != b) or (a == b and math.copysign(1.0, a) == math.copysign(1.0, b))
+
+
+def test_special_values():
+    inf, nan = math.inf, math.nan
+    S = [0.0, -0.0, 1.0, -1.0, 0.5, -2.0, inf, -inf, nan, 5e-324, 1e300, -1e300, math.pi, 1e22]
+    unary = {"sin": math.sin, "cos": math.cos, "tan": math.tan, "atan": math.atan, "asin": math.asin, "acos": math.acos}
+    for name, f in unary.items():
+        got = _native.cpu_libm(name, np.array(S))
+        for v, g in zip(S, got):
+            try:
+                ref = f(v)
+            except ValueError:
+                ref = nan
+            if name in ("sin", "cos", "tan") and abs(v) >= 1e22:   # glibc is not correctly rounded everywhere there
+                ref = float(getattr(mpmath, name)(mpmath.mpf(v))) if math.isfinite(v) else ref
+            assert _same(g, ref), (name, v, g, ref)
+    binary = {"atan2": math.atan2, "hypot": math.hypot}
+    for name, f in binary.items():
+        xs, ys = np.array([a for a in S for _ in S]), np.array([b for _ in S for b in S])
+        got = _native.cpu_libm(name, xs, ys)
+        for a, b, g in zip(xs, ys, got):
+            assert _same(g, f(a, b)), (name, a, b, g)
+    # pow: C99 Annex F (Python's math.pow raises where C returns +-inf)
+    cases = [(0.0, -1.0, inf), (-0.0, -1.0, -inf), (-0.0, -2.0, inf), (0.0, 1.5, 0.0), (-0.0, 3.0, -0.0),
+             (-8.0, 1.0 / 3.0, nan), (-2.0, 3.0, -8.0), (nan, 0.0, 1.0), (1.0, nan, 1.0), (2.0, inf, inf),
+             (0.5, inf, 0.0), (-inf, 3.0, -inf), (inf, -1.0, 0.0), (1e300, 1.5, inf), (1e-300, 1.5, 1e-450),
+             (4.0, 1.5, 8.0), (3.0, 2.0, 9.0), (2.0, 0.5, math.sqrt(2.0))]
+    for a, b, ref in cases:
+        g = _native.cpu_libm("pow", np.array([a]), np.array([b]))[0]
+        assert _same(g, ref), ("pow", a, b, g, ref)

@@ -8,6 +8,10 @@
 #     configs  bench lines of configs A, B, C, E and the batch sweep 1024 / 4096
 #     kernels  hybrid A* and point-formulation throughput
 #     ws2      2-rank rehearsal of the multi-GPU bench on one GPU (gloo: RCCL refuses two ranks on one device)
+#     pytest:FILE[,FILE...]   only these GPU test files (tests/FILE)
+#     benchC / benchE / benchD20   config C at 6 steps, config E, config D at 20 steps
+#     pmcC / pmcE    PMC passes for configs C / E only
+#     stall    the three SQ stall passes (tools/gpu_stall.sh) on config D
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
@@ -42,6 +46,14 @@ for S in "$@"; do
              run points 300 python -u tools/bench_points.py ;;
     ws2) HTP_DIST_BACKEND=gloo run ws2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
            --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --batch 4096 --steps 2 --waves 512 --gen-procs 8 ;;
+    pytest:*) files=$(echo "${S#pytest:}" | tr ',' ' ' | sed 's|\([^ ]*\)|tests/\1|g')
+              run pytest_sel 900 python -u -m pytest $files -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    benchC) run benchC 600 python -u bench.py --config C --steps 6 --no-cpu-baseline ;;
+    benchE) run benchE 900 python -u bench.py --config E --steps 1 --warmup 0 --no-cpu-baseline ;;
+    benchD20) run benchD20 900 python -u bench.py --steps 20 --no-cpu-baseline ;;
+    pmcC) bash tools/gpu_pmc.sh ${T}C --config C --batch 4096 || exit 1 ;;
+    pmcE) bash tools/gpu_pmc.sh ${T}E --config E --batch 1024 || exit 1 ;;
+    stall) bash tools/gpu_stall.sh ${T}D || exit 1 ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done

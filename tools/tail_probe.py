@@ -2,7 +2,8 @@
 order by 1 024 wavefronts), read every problem's cycle count, and replay the claim order as list scheduling
 (each ticket goes to the first free wavefront).  makespan / (sum / waves) - 1 is the tail + imbalance share.
 
-Usage: python tools/tail_probe.py [config] [batch] [cache_dir]"""
+Usage: python tools/tail_probe.py [config] [batch] [cache_dir] [save.npz]
+The optional npz keeps every problem's cycle count, iterations and status for tools/scale_projection.py."""
 import heapq
 import json
 import os
@@ -40,3 +41,6 @@ out = {"config": cfg, "batch": B, "waves": waves, "kernel_ms": kms,
                            "status": int(res.status[p])} for p in order[:8]],
        "cycles_per_ms": makespan / kms}
 print(json.dumps(out, indent=1))
+if len(sys.argv) > 4:
+    np.savez_compressed(sys.argv[4], cycles=cyc, iterations=res.iterations, status=res.status, waves=waves,
+                        kernel_ms=kms, cycles_per_ms=makespan / kms)
