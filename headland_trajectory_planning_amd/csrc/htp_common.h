@@ -10,6 +10,11 @@
 #error "define HTP_HD (__host__ __device__ or empty) before including htp_common.h"
 #endif
 
+// obca_core.h LocalStore: factored local blocks kept for the KKT solves (experiment, off; see there)
+#ifndef HTP_STORE_LOCAL
+#define HTP_STORE_LOCAL 0
+#endif
+
 namespace htp {
 
 constexpr int NS = 5;       // state  [x, y, v, theta, steer]
@@ -203,7 +208,7 @@ inline Layout make_layout(const Dims& d) {
   L.plist = take(d.P);
   // LocalStore<MAXE, MAXE>::COUNT fields per local block (the widest kernel instance; obca_core.h)
   constexpr int64_t LF_MAX = (2 * MAXE + 2) * (2 * MAXE + 3) / 2 + 3 * (2 * MAXE + 2) + 2 * (2 * MAXE) + 2 + 4 + 1;
-  L.lfac = take(d.form == 0 ? LF_MAX * d.P : 0);
+  L.lfac = take(HTP_STORE_LOCAL && d.form == 0 ? LF_MAX * d.P : 0);
   L.total = o;
   return L;
 }

@@ -42,6 +42,14 @@
 #else
 #define HTP_PHASE HTP_FI
 #endif
+// The barrier function (a log per bounded variable and slack, 8 loads per lane in flight) is evaluated at the
+// current point and at each line-search trial point from three sites; one out-of-line copy instead of three
+// inlined ones removes a sixth of the kernel's instructions (tools/code_size.py).
+#ifndef HTP_BARRIER_INLINE
+#define HTP_BARRIER_ATTR __attribute__((noinline))
+#else
+#define HTP_BARRIER_ATTR HTP_FI
+#endif
 
 namespace htp {
 
@@ -136,14 +144,11 @@ struct LocalBlock {
   }
 };
 
-// Factored local blocks kept for the KKT solves (HTP_STORE_LOCAL): the factor sweep stores every unpivoted
-// block's LDL^T factor and the rows the solves read, structure-of-arrays (field f of block p at f * P + p, so a
-// wave's 64 blocks load as one coalesced 512-byte access per field); the right-hand-side and back sweeps of every
-// KKT solve with that factorization (the step, its second-order corrections) load them instead of rebuilding
-// and refactoring each block.  The same doubles either way.
-#ifndef HTP_STORE_LOCAL
-#define HTP_STORE_LOCAL 1
-#endif
+// Factored local blocks kept for the KKT solves (HTP_STORE_LOCAL, experiment, off): the factor sweep stores every
+// unpivoted block's LDL^T factor and the rows the solves read, structure-of-arrays (field f of block p at f * P + p);
+// the right-hand-side and back sweeps load them instead of rebuilding and refactoring each block.  The same doubles
+// either way, but 107 extra doubles per block written and read twice per iteration cost more than the VALU they
+// save: 23 % more cycles per IPM iteration on config D (profiles/r04c_ab_D.txt, base vs sl0).
 template <int EN, int EM>
 struct LocalStore {
   static constexpr int NZ = EN + EM, NL = NZ + 2, NPK = NL * (NL + 1) / 2;
@@ -568,8 +573,7 @@ struct ObcaSolver {
         w[1] += a1[j] * lx[j];
       }
     }
-    cs = cos(th);
-    sn = sin(th);
+    dyn_sincos(th, sn, cs);
   }
 
   // point formulation: obstacle halfspaces, lam, w = A'lam and the pose of block p
@@ -596,8 +600,7 @@ struct ObcaSolver {
       G.w1 += G.A1[j] * G.lam[j];
     }
     const double th = x[NS * G.i + 3];
-    G.cs = cos(th);
-    G.sn = sin(th);
+    dyn_sincos(th, G.sn, G.cs);
     G.tx = x[NS * G.i];
     G.ty = x[NS * G.i + 1];
   }
@@ -3855,7 +3858,7 @@ struct ObcaSolver {
 
   // barrier function at (x, s[, R]); +inf if a slack is not positive.  resto_obj: the restoration
   // problem's objective and n/p barrier terms, else the original sf * f
-  HTP_HD HTP_PHASE double barrier(const gd* x, const gd* s, const gd* Rv, double mu_, bool resto_obj) const {
+  HTP_BARRIER_ATTR HTP_HD double barrier(const gd* x, const gd* s, const gd* Rv, double mu_, bool resto_obj) const {
     const gd* xL = A(L.xL); const gd* xU = A(L.xU);
     const gd* dL = A(L.dL); const gd* dU = A(L.dU);
     const double kd = o.kappa_d * mu_;

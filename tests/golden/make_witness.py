@@ -1,0 +1,62 @@
+"""Oracle self-divergence witnesses for the fixtures where the device and the oracle fixture part ways
+inside long restoration cycles (tests/test_gpu_obca.py FAILURE_CLASS_ONLY / DIVERGENT_AFTER_RESTORATION,
+tests/test_gpu_points.py CHAOTIC): the same oracle (oracle/ipm.py, IPOPT 3.14 restated) on the same instance
+with a second, equally valid elimination order of the same KKT systems (StructuredKKTLoop for the full-size
+fixtures, StructuredPointKKT for the point formulation, whose fixtures use DenseKKT).  Where the two orders
+already end at different statuses or points, the reference algorithm itself does not determine the outcome at
+rounding level, and the device's different-but-valid ending is the same phenomenon.
+
+    python tests/golden/make_witness.py D347 E84 E6 P19     -> tests/golden/witness/<name>.npz
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+OUT = os.path.join(ROOT, "tests", "golden", "witness")
+
+
+def run(name):
+    from oracle.ipm import IpoptRestatement
+    t = time.time()
+    if name.startswith("P"):   # point formulation, tests/test_gpu_points.py small instances (N=12, M=2)
+        from headland_trajectory_planning_amd import synth
+        from oracle.nlp_points import PointNLP
+        from oracle.structured import StructuredPointKKT
+        inst = synth.make_points_instance(int(name[1:]), N=12, M=2)
+        nlp = PointNLP(inst)
+        a = IpoptRestatement(nlp).solve()
+        b = IpoptRestatement(nlp, kkt=StructuredPointKKT(nlp)).solve()
+        orders = ("DenseKKT", "StructuredPointKKT")
+        N = 12
+    else:
+        from _fixture_io import load_instance
+        from oracle.nlp import ObcaNLP
+        from oracle.structured import StructuredKKT, StructuredKKTLoop
+        g = np.load(os.path.join(ROOT, "tests", "golden", "obca_full", f"{name}.npz"))
+        inst = load_instance(g)
+        nlp = ObcaNLP(inst)
+        a = {"x": np.concatenate([g["states"], np.zeros(1)]), "status": int(g["status"]), "iters": int(g["iters"]),
+             "n_resto": int(g["n_resto"]), "f": float(g["f"])}   # the fixture itself (StructuredKKT)
+        b = IpoptRestatement(nlp, kkt=StructuredKKTLoop(nlp)).solve()
+        orders = ("StructuredKKT", "StructuredKKTLoop")
+        N = int(g["N"])
+    os.makedirs(OUT, exist_ok=True)
+    np.savez(os.path.join(OUT, f"{name}.npz"), orders=np.array(orders),
+             states_a=a["x"][:5 * N], status_a=a["status"], iters_a=a["iters"], n_resto_a=a["n_resto"],
+             states_b=b["x"][:5 * N], status_b=b["status"], iters_b=b["iters"], n_resto_b=b["n_resto"],
+             seconds=time.time() - t)
+    d = float(np.max(np.abs(a["x"][:5 * N] - b["x"][:5 * N])))
+    return (f"{name}: {orders[0]} status {a['status']} it {a['iters']} resto {a['n_resto']} | {orders[1]} status "
+            f"{b['status']} it {b['iters']} resto {b['n_resto']} | max state diff {d:.3g} ({time.time() - t:.0f} s)")
+
+
+if __name__ == "__main__":
+    import multiprocessing as mp
+    with mp.Pool(min(4, len(sys.argv) - 1)) as pool:
+        for line in pool.imap_unordered(run, sys.argv[1:]):
+            print(line, flush=True)

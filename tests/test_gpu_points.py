@@ -32,10 +32,35 @@ def _feasible(inst, x, tol=1e-6):
             and np.all(c[~eq] <= nlp.g_U[~eq] + tol))
 
 
+def _stationarity(nlp, x, tol_act=1e-3):
+    """Least-squares dual residual of the NLP at x (equality + active inequality rows and bounds), relative."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    g = nlp.cons(x)
+    act = (nlp.g_L == nlp.g_U) | (np.abs(g - nlp.g_L) <= tol_act) | (np.abs(g - nlp.g_U) <= tol_act)
+    J = sp.csr_matrix(nlp.jac(x))[act]
+    bl = np.isfinite(nlp.x_L) & (np.abs(x - nlp.x_L) <= tol_act)
+    bu = np.isfinite(nlp.x_U) & (np.abs(x - nlp.x_U) <= tol_act)
+    E = sp.identity(len(x), format="csr")
+    A = sp.vstack([J, E[bl], E[bu]]).T.tocsr()
+    gf = nlp.grad_f(x)
+    y = spla.lsqr(A, -gf, atol=1e-14, btol=1e-14, iter_lim=20000)[0]
+    return np.max(np.abs(gf + A @ y)) / max(1.0, np.max(np.abs(gf)))
+
+
+WITNESS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "witness")
+# Restoration cycles the reference algorithm does not determine at rounding level: the oracle itself, with the
+# structured elimination order of the same KKT systems (StructuredPointKKT), ends 3.4 away from its dense-KKT
+# run (177 vs 234 iterations; tests/golden/witness/P19.npz, tests/golden/make_witness.py).  The device must
+# end with the oracle's status at a KKT point of the same NLP.  Every other restoration case: state parity.
+CHAOTIC = {19: "P19"}
+
+
 def test_gpu_matches_oracle_quads(ctx):
     """24 small problems against the oracle (ground truth): same status; without a restoration phase
     the same iteration count (+-1) and states within 1e-6; through restoration (optimizer_points.py:157-191
-    hands IPOPT the same NLP) states within the north_star tolerance 1e-4 and a feasible point."""
+    hands IPOPT the same NLP) states within the north_star tolerance 1e-4 -- except the pinned CHAOTIC cases,
+    where the oracle's own two elimination orders disagree (witness fixture), checked at the KKT level."""
     insts = [synth.make_points_instance(pid, N=12, M=2) for pid in range(24)]
     g = ctx.solve_points(_native.PointsPackedBatch(insts))
     bad = []
@@ -45,6 +70,11 @@ def test_gpu_matches_oracle_quads(ctx):
         ok = g.status[k] == ref["status"]
         if ok and ref["n_resto"] == 0 and g.n_resto[k] == 0:
             ok = abs(int(g.iterations[k]) - ref["iters"]) <= 1 and err < 1e-6
+        elif ok and g.status[k] in (0, 1) and k in CHAOTIC:
+            w = np.load(os.path.join(WITNESS, CHAOTIC[k] + ".npz"))
+            assert int(w["status_a"]) == ref["status"] and int(w["iters_a"]) == ref["iters"]   # the fixture is this run
+            assert np.max(np.abs(w["states_a"] - w["states_b"])) > 1e-4                        # the witness holds
+            ok = _feasible(inst, g.x[k]) and _stationarity(PointNLP(inst), g.x[k]) <= 1e-5
         elif ok and g.status[k] in (0, 1):
             ok = err <= 1e-4 and _feasible(inst, g.x[k])
         if not ok:

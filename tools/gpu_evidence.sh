@@ -12,6 +12,10 @@
 #     benchC / benchE / benchD20   config C at 6 steps, config E, config D at 20 steps
 #     pmcC / pmcE    PMC passes for configs C / E only
 #     stall    the three SQ stall passes (tools/gpu_stall.sh) on config D
+#     diag     I-cache / TLB / L2 / L1 passes (tools/gpu_diag.sh) on config D
+#     ab:CFG:B:name,name...   A/B of libhtp_<name>.so variants (tools/build_variants.py; "base" = libhtp.so)
+#     counters  rocprofv3 --list-avail (the PMC counter names of this box)
+#     tail      tools/tail_probe.py on config D 32768 (per-problem cycles -> TAG_tail_D.npz for scale_projection.py)
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
@@ -54,6 +58,12 @@ for S in "$@"; do
     pmcC) bash tools/gpu_pmc.sh ${T}C --config C --batch 4096 || exit 1 ;;
     pmcE) bash tools/gpu_pmc.sh ${T}E --config E --batch 1024 || exit 1 ;;
     stall) bash tools/gpu_stall.sh ${T}D || exit 1 ;;
+    diag) bash tools/gpu_diag.sh ${T}D || exit 1 ;;
+    ab:*) IFS=: read -r _ cfg nb names <<< "$S"
+          run ab_$cfg 900 python -u tools/ab_phase.py $cfg $nb $(echo $names | tr ',' ' ') ;;
+    counters) run counters 120 rocprofv3 --list-avail ;;
+    tail) run tailgen 300 python -u bench.py --gen-only --cache /tmp/htp_instcache
+          run tail 600 python -u tools/tail_probe.py D 32768 /tmp/htp_instcache gpurun_out/${T}_tail_D.npz ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done
