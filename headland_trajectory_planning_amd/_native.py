@@ -190,11 +190,13 @@ def _declare(lib):
     lib.htp_libm_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int32] + [ctypes.c_void_p] * 3 + \
         [ctypes.c_int64, ctypes.c_void_p]
     lib.htp_libm_batch_device.restype = ctypes.c_int
+    lib.htp_mfma_f64_probe.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_void_p]
+    lib.htp_mfma_f64_probe.restype = ctypes.c_int
     return lib
 
 
 # correctly rounded libm of the planner cores (csrc/htp_libm.h): function ids of htp_libm_batch_device
-LIBM_FN = {"sin": 0, "cos": 1, "tan": 2, "atan": 3, "atan2": 4, "asin": 5, "acos": 6, "hypot": 7, "pow": 8}
+LIBM_FN = {"sin": 0, "cos": 1, "tan": 2, "atan": 3, "atan2": 4, "asin": 5, "acos": 6, "hypot": 7, "pow": 8, "log": 9}
 LIBM_BINARY = {"atan2", "hypot", "pow"}
 CPU_LIB_PATH = os.path.join(HERE, "libhtp_cpu.so")
 _CPU_LIB = None
@@ -909,6 +911,23 @@ class Context:
                                             ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"[htp] htp_libm_batch_device failed: {self.error()}")
+        s.synchronize()
+        return out.cpu().numpy()
+
+    def mfma_f64(self, A, B, C):
+        """htp_mfma_f64_probe over host tiles A [n,16,4], B [n,4,16], C [n,16,16] -> D [n,16,16]."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        t = [torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64)).to(dev) for v in (A, B, C)]
+        n = t[0].shape[0]
+        if t[0].shape != (n, 16, 4) or t[1].shape != (n, 4, 16) or t[2].shape != (n, 16, 16):
+            raise ValueError("[htp] mfma_f64: tiles must be [n,16,4], [n,4,16], [n,16,16]")
+        out = torch.empty_like(t[2])
+        s = torch.cuda.current_stream(dev)
+        rc = self.lib.htp_mfma_f64_probe(self.ctx, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), out.data_ptr(),
+                                         n, ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"[htp] htp_mfma_f64_probe failed: {self.error()}")
         s.synchronize()
         return out.cpu().numpy()
 

@@ -145,10 +145,9 @@ HTP_HD inline void prep(const double* rows, int n, int N, double dT, double wb, 
   rp_params[2] = Lp / (2.0 * N - 2.0);   // ds / 2 (synth.make_orchard_instance)
 }
 
-// ---- resample (synth._resample_rows) + the headland width the warm start needs (lane 0)
-// ref: [nr][5] init-guess rows; s: nr scratch doubles; traj: [N][5] out.  Returns hw.
-HTP_HD inline double resample_hw(const double* ref, int nr, int N, double* s, double* traj, const Vehicle& V,
-                                 const oge::Scene& S, double margin) {
+// ---- resample (synth._resample_rows): init-guess rows -> N rows at even arc length (one lane)
+// ref: [nr][5] init-guess rows; s: nr scratch doubles; traj: [N][5] out.
+HTP_HD inline void resample(const double* ref, int nr, int N, double* s, double* traj) {
   s[0] = 0.0;
   for (int i = 1; i < nr; ++i) s[i] = s[i - 1] + hm::hypot(ref[5 * i] - ref[5 * (i - 1)], ref[5 * i + 1] - ref[5 * (i - 1) + 1]);
   const double send = s[nr - 1];
@@ -177,6 +176,12 @@ HTP_HD inline double resample_hw(const double* ref, int nr, int N, double* s, do
   traj[2] = 0.0;
   traj[5 * (N - 1) + 2] = 0.0;
   traj[4] = 0.0;
+}
+
+// ---- resample + the headland width the warm start needs (lane 0).  Returns hw.
+HTP_HD inline double resample_hw(const double* ref, int nr, int N, double* s, double* traj, const Vehicle& V,
+                                 const oge::Scene& S, double margin) {
+  resample(ref, nr, N, s, traj);
   // _needed_headland over the footprint at the N resampled poses and every init-guess row
   const double ang = oge::headland_angle(S, oge::NEAR);
   double ys[oge::MAXR], xs[oge::MAXR];

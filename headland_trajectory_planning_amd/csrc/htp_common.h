@@ -15,6 +15,11 @@
 #define HTP_STORE_LOCAL 0
 #endif
 
+// obca_core.h ObcaSolver::ubx / ubs: skip the loads of upper-bound data that is +inf / 0 for the whole solve
+#ifndef HTP_UB_SKIP
+#define HTP_UB_SKIP 0
+#endif
+
 namespace htp {
 
 constexpr int NS = 5;       // state  [x, y, v, theta, steer]

@@ -80,3 +80,34 @@ extern "C" int htp_cpu_libm_batch(int32_t fn, const double* x, const double* y, 
   for (int64_t i = 0; i < n; ++i) out[i] = htp::hm::eval(fn, x[i], y ? y[i] : 0.0);
   return 0;
 }
+
+// The notebook chain's heuristic lowering (ychain_core.h), host build: waypoints, guide rows, lane rings and
+// search lengths of one problem (tests/test_ychain_cpu.py compares it with path_planner's ReferenceLineHeuristic).
+#include "ychain_core.h"
+
+extern "C" int htp_cpu_ychain_lower(const double* rows, int32_t nrows, const double* eps, const double* start,
+                                    const double* goal, double drive_row_offset, double default_len, double* wp,
+                                    int32_t* n_wp, double* guide, int32_t cap_guide, int32_t* n_guide, double* rings,
+                                    int32_t* n_ring, double* lengths) {
+  if (nrows < 1 || nrows > htp::yc::MAXROWS) return -1;
+  double w[htp::yc::MAXWP][2];
+  const int n = htp::yc::waypoints(rows, nrows, eps, start, goal, drive_row_offset, w);
+  if (n < 2) return 1;
+  *n_wp = n;
+  for (int k = 0; k < n; ++k) { wp[2 * k] = w[k][0]; wp[2 * k + 1] = w[k][1]; }
+  const int m = htp::yc::guide(w, n, guide, cap_guide);
+  if (m < 0) return 2;
+  *n_guide = m;
+  for (int k = 0; k + 1 < n; ++k) {
+    double ring[htp::yc::CAPV][2];
+    const int nv = htp::yc::capsule(w[k], w[k + 1], htp::yc::LANE_HALF_WIDTH, ring);
+    if (nv < 3) return 3;
+    n_ring[k] = nv;
+    for (int j = 0; j < nv; ++j) {
+      rings[(k * htp::yc::CAPV + j) * 2] = ring[j][0];
+      rings[(k * htp::yc::CAPV + j) * 2 + 1] = ring[j][1];
+    }
+    lengths[k] = htp::yc::search_length(k, n - 1, default_len);
+  }
+  return 0;
+}

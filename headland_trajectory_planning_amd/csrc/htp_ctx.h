@@ -48,6 +48,10 @@ struct htp_ctx {
   void* ch_ws = nullptr;
   size_t ch_ws_bytes = 0;
   hipEvent_t ch_ev0 = nullptr, ch_ev1 = nullptr;
+  // notebook planner chain (htp_ychain.hip): stage boundaries Y-park | lowering | hybrid A* | init guess
+  void* yc_ws = nullptr;
+  size_t yc_ws_bytes = 0;
+  hipEvent_t yc_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
 static inline int fail(htp_ctx* c, const std::string& m) {

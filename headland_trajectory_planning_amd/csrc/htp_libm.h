@@ -43,6 +43,8 @@ inline double asin(double x) { return std::asin(x); }
 inline double acos(double x) { return std::acos(x); }
 inline double hypot(double x, double y) { return std::hypot(x, y); }
 inline double pow(double x, double y) { return std::pow(x, y); }
+inline double log(double x) { return std::log(x); }
+inline void sincos(double x, double& s, double& c) { s = std::sin(x); c = std::cos(x); }
 #else
 
 // ---- constants (tools/gen_libm_consts.py)
@@ -472,6 +474,27 @@ HTP_HD inline double exp_dd(dd a) {        // rounded exp(a); normal results cor
   dd E = mul(r, p);                        // expm1(r / 32)
   for (int j = 0; j < 5; ++j) E = add(mul_d(E, 2.0), mul(E, E));   // expm1(2 z) = 2 E + E^2
   return std::ldexp(round_dd(add_d(E, 1.0)), (int)k);
+}
+HTP_HD inline double log(double x) {
+  if (x != x) return x;
+  if (x < 0.0) return (x - x) / (x - x);
+  if (x == 0.0) return -__builtin_huge_val();
+  if (x == __builtin_huge_val()) return x;
+  if (x == 1.0) return 0.0;
+  return round_dd(log_dd(x));
+}
+// sin and cos of one argument, one reduction: the same doubles as sin(x), cos(x)
+HTP_HD inline void sincos(double x, double& s, double& c) {
+  if (nonfinite(x)) { s = c = x - x; return; }
+  if (std::fabs(x) < 0x1p-27) { s = x; c = 1.0; return; }
+  int q;
+  const dd r = reduce_pio2(x, q);
+  const dd sr = sin_dd(r), cr = cos_dd(r);
+  dd vs = (q & 1) ? cr : sr, vc = (q & 1) ? sr : cr;
+  if (q & 2) vs = neg(vs);
+  if (((q + 1) & 2) != 0) vc = neg(vc);
+  s = round_dd(vs);
+  c = round_dd(vc);
 }
 HTP_HD inline bool is_int(double y) { return rint(y) == y; }
 HTP_HD inline bool is_odd_int(double y) { return is_int(y) && std::fabs(y) < 0x1p53 && std::fmod(y, 2.0) != 0.0; }

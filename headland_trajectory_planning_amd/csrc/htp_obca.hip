@@ -216,6 +216,9 @@ void htp_destroy(htp_ctx* c) {
   if (c->ch_ws) (void)hipFree(c->ch_ws);
   if (c->ch_ev0) (void)hipEventDestroy(c->ch_ev0);
   if (c->ch_ev1) (void)hipEventDestroy(c->ch_ev1);
+  if (c->yc_ws) (void)hipFree(c->yc_ws);
+  for (auto e : c->yc_ev)
+    if (e) (void)hipEventDestroy(e);
   delete c;
 }
 

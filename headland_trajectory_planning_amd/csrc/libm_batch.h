@@ -7,7 +7,7 @@
 namespace htp {
 namespace hm {
 
-enum { F_SIN = 0, F_COS, F_TAN, F_ATAN, F_ATAN2, F_ASIN, F_ACOS, F_HYPOT, F_POW, F_COUNT };
+enum { F_SIN = 0, F_COS, F_TAN, F_ATAN, F_ATAN2, F_ASIN, F_ACOS, F_HYPOT, F_POW, F_LOG, F_COUNT };
 
 HTP_HD inline double eval(int fn, double x, double y) {
   switch (fn) {
@@ -20,6 +20,7 @@ HTP_HD inline double eval(int fn, double x, double y) {
     case F_ACOS: return acos(x);
     case F_HYPOT: return hypot(x, y);
     case F_POW: return pow(x, y);
+    case F_LOG: return log(x);
     default: return __builtin_nan("");
   }
 }

@@ -17,6 +17,49 @@
 #include <cmath>
 
 #include "htp_common.h"
+#include "htp_libm.h"
+
+// The solver's transcendental functions (dynamics sin / cos / tan, barrier log, IPOPT's pow updates).  With
+// HTP_SOLVER_CRLIBM (default) they are the correctly rounded htp_libm.h functions on the device and on every
+// host build, so the device solve is reproducible bit for bit on the host (the emulation of csrc/emu_wave.h,
+// tests/test_gpu_emulation.py); 0 takes the platform's (ocml on the device).
+#ifndef HTP_SOLVER_CRLIBM
+#define HTP_SOLVER_CRLIBM 1
+#endif
+namespace htp {
+namespace sm {
+#if HTP_SOLVER_CRLIBM
+using hm::cos;
+using hm::log;
+using hm::pow;
+using hm::sin;
+using hm::sincos;
+using hm::tan;
+#else
+HTP_HD inline double sin(double x) { return ::sin(x); }
+HTP_HD inline double cos(double x) { return ::cos(x); }
+HTP_HD inline double tan(double x) { return ::tan(x); }
+HTP_HD inline double log(double x) { return ::log(x); }
+HTP_HD inline double pow(double x, double y) { return ::pow(x, y); }
+HTP_HD inline void sincos(double x, double& s, double& c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  ::sincos(x, &s, &c);
+#else
+  s = ::sin(x);
+  c = ::cos(x);
+#endif
+}
+#endif
+}  // namespace sm
+}  // namespace htp
+
+// Contraction: a * b + c fused exactly where the source writes it within one expression (clang's llvm.fmuladd),
+// never across statements -- the same fused operations in the device build and in the clang host emulation
+// (emu_wave.h).  htp_libm.h above leaves contract(off) in effect; this restores it for the solver.
+#if defined(__clang__)
+#pragma clang fp contract(on)
+#endif
+
 #include "dyn_gen.h"
 
 #ifndef HTP_UNROLL_N
@@ -50,6 +93,16 @@
 #else
 #define HTP_BARRIER_ATTR HTP_FI
 #endif
+
+#ifndef HTP_RELAX_RICCATI
+#define HTP_RELAX_RICCATI 1   // 0: experiments only -- relaxed systems take the block LDL^T path (round 2)
+#endif
+#ifndef HTP_PT_RICCATI
+#define HTP_PT_RICCATI 1      // 0: experiments only -- the point formulation takes the block LDL^T path
+#endif
+// FORM 0 with the relaxed-dynamics Riccati (HTP_RELAX_RICCATI) never takes the block LDL^T path, so its stage
+// assembly stores only what the Riccati records read (the w x w Hessian block, the jerk cross terms, J_i).
+#define HTP_COMPACT_STAGE HTP_RELAX_RICCATI
 
 namespace htp {
 
@@ -395,6 +448,12 @@ struct ObcaSolver {
   HTP_HD HTP_FI static const gd* gp(const double* p) { return (const gd*)p; }
   HTP_HD HTP_FI double par(int k) const { return gp(in.par)[k]; }
   HTP_HD HTP_FI double tauv(const gd* x, int i) const { return D.topt ? x[D.oTAU + i] : 1.0; }
+  // Upper bounds that exist (HTP_UB_SKIP): optimizer.py's multipliers mu, lambda ([oMU, oTAU), :292-354) have a
+  // lower bound only and the distance rows c3 (odd inequality rows, :414-425) no upper bound, so x_U / d_U stay
+  // +inf and z_U / dz_U / v_U stay exactly 0 for the whole solve (never relaxed, corrected or stepped).  Passes
+  // over n and m_in read those arrays only where the bound exists; every value they skip is that constant.
+  HTP_HD HTP_FI bool ubx(int q) const { return PT || !HTP_UB_SKIP || q < D.oMU || q >= D.oTAU; }
+  HTP_HD HTP_FI bool ubs(int r) const { return PT || !HTP_UB_SKIP || (r & 1) == 0; }
 
   // Lane-blocked sweep over [0, n): per trip a lane takes SW_U indices q_k = b + k*width.
   // ld(q, k) gathers element q into register slot k with the index clamped into range,
@@ -1933,8 +1992,11 @@ struct ObcaSolver {
         add(NS + k, NS + k, st * st / Et);
       }
     }
-    for (int r = 0; r < NBMAX; ++r)
-      for (int q = 0; q < NBMAX; ++q)
+    // the Riccati path reads only the w x w block [NS, nb)^2 of K (riccati_factor[_mfma]); the block LDL^T
+    // path (point formulation, experiments) reads all of it
+    constexpr int R0 = (!PT && HTP_COMPACT_STAGE) ? NS : 0;
+    for (int r = R0; r < NBMAX; ++r)
+      for (int q = R0; q < NBMAX; ++q)
         if (r < nb && q < nb) K[r * nb + q] = Kl[r >= q ? r * (r + 1) / 2 + q : q * (q + 1) / 2 + r];
     // Riccati records: reciprocal scaling of this stage's multiplier rows
     {
@@ -1945,14 +2007,22 @@ struct ObcaSolver {
     // off-diagonal block for i+1 (rows of block i+1, cols of block i)
     if (i < N - 1) {
       gd* O = A(L.Off) + (int64_t)(i + 1) * nb * nb;
-      for (int q = 0; q < nb * nb; ++q) O[q] = 0.0;
+      constexpr bool compact = !PT && HTP_COMPACT_STAGE;
+      if (compact) {   // the Riccati reads only the jerk cross terms C (rows U0, U0+1; columns U0, U0+1, T0) of Off
+        const int U0 = NS + 5;
+        for (int a = 0; a < 2; ++a)
+          for (int b = 0; b < 3; ++b) O[(U0 + a) * nb + U0 + b] = 0.0;
+      } else {
+        for (int q = 0; q < nb * nb; ++q) O[q] = 0.0;
+      }
       double w[8], J[40];
       stage_w(x, i, w);
       dynJ(w, J);
       gd* Js = A(L.LD) + (int64_t)i * nb * nb + JOFF;  // unscaled J_i (stride 8) for the Riccati records
       for (int k = 0; k < NS; ++k) {
         const double s_ = scE[D.eDyn + NS * i + k];
-        for (int j = 0; j < D.nw; ++j) O[k * nb + NS + j] = -s_ * J[k * D.nw + j];
+        if (!compact)
+          for (int j = 0; j < D.nw; ++j) O[k * nb + NS + j] = -s_ * J[k * D.nw + j];
         for (int j = 0; j < 8; ++j) Js[k * 8 + j] = (j < D.nw) ? J[k * D.nw + j] : 0.0;
       }
       if (PT && !ls && i < N - 2) {
@@ -2489,7 +2559,7 @@ struct ObcaSolver {
     return bad;
   }
 
-#if defined(__HIPCC__)
+#if defined(__HIPCC__) || defined(HTP_EMU_WAVE)
   // ------------------------------------------------ Riccati recursion on the matrix core
   // Same recursion as riccati_factor / riccati_solve, written as 16x16 fp64 MFMA tiles over the
   // augmented stage variables u_i = [z_i (rows 0..7, z = [x, u_{i-1}, tau_{i-1}] zero-padded to 8) ;
@@ -3248,7 +3318,7 @@ struct ObcaSolver {
   // then Z = K^-1 (r_Z - C' y_T).  Inertia (Sylvester, Schur on y_T): the 5 terminal negatives iff
   // S_T Sig S_T + E_T is positive definite.  Sig = five solves with unit right-hand sides at x_{N-1}.
   HTP_HD HTP_FI void ric_solve(const gd* V, gd* X) {
-#if defined(__HIPCC__)
+#if defined(__HIPCC__) || defined(HTP_EMU_WAVE)
     if constexpr (Ctx::kMfma) { riccati_solve_mfma(V, X); return; }
 #endif
     riccati_solve(V, X);
@@ -3261,7 +3331,7 @@ struct ObcaSolver {
     gd* rec = A(L.fac) + (int64_t)N * nb * nb;
     const gd* scE = A(L.scE);
     const gd* eR = A(L.eR);
-#if defined(__HIPCC__)
+#if defined(__HIPCC__) || defined(HTP_EMU_WAVE)
     if constexpr (Ctx::kMfma) {
       riccati_sigma_mfma(rec + 20);       // all five columns in one pair of passes
     } else
@@ -3352,16 +3422,10 @@ struct ObcaSolver {
     // delta_c > 0 and the restoration phase relax the dynamics rows: the same recursion through
     // relax_P.  The point formulation's hard terminal rows (block N) enter through their 5 x 5 Schur
     // complement (terminal_schur).
-#ifndef HTP_RELAX_RICCATI
-#define HTP_RELAX_RICCATI 1   // 0: experiments only -- relaxed systems take the block LDL^T path (round 2)
-#endif
-#ifndef HTP_PT_RICCATI
-#define HTP_PT_RICCATI 1      // 0: experiments only -- the point formulation takes the block LDL^T path
-#endif
     if ((!PT || HTP_PT_RICCATI) && (HTP_RELAX_RICCATI || (dc == 0.0 && !rs))) {
       int bad;
       ric_relax = dc != 0.0 || rs;
-#if defined(__HIPCC__)
+#if defined(__HIPCC__) || defined(HTP_EMU_WAVE)
       if constexpr (Ctx::kMfma) bad = riccati_factor_mfma(dc);
       else
 #endif
@@ -3658,7 +3722,7 @@ struct ObcaSolver {
     const bool two = e2 != nullptr;
     {
       double g_[SW_U], zl_[SW_U], zu_[SW_U], x_[SW_U], xl_[SW_U], xu_[SW_U];
-      sweep(D.n, [&](int q, int k) { g_[k] = gl[q]; zl_[k] = zL[q]; zu_[k] = zU[q]; x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; },
+      sweep(D.n, [&](int q, int k) { g_[k] = gl[q]; zl_[k] = zL[q]; zu_[k] = ubx(q) ? (double)zU[q] : 0.0; x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = ubx(q) ? (double)xU[q] : HTP_INF; },
             [&](int, int k) {
               dual = dmax(dual, dabs(g_[k] - zl_[k] + zu_[k]));
               if (finite_(xl_[k])) {
@@ -3675,7 +3739,7 @@ struct ObcaSolver {
     }
     {
       double yd_[SW_U], vl_[SW_U], vu_[SW_U], s_[SW_U], dl_[SW_U], du_[SW_U], d_[SW_U];
-      sweep(D.md, [&](int r, int k) { yd_[k] = yd[r]; vl_[k] = vL[r]; vu_[k] = vU[r]; s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = dU[r]; d_[k] = dd[r]; },
+      sweep(D.md, [&](int r, int k) { yd_[k] = yd[r]; vl_[k] = vL[r]; vu_[k] = ubs(r) ? (double)vU[r] : 0.0; s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = ubs(r) ? (double)dU[r] : HTP_INF; d_[k] = dd[r]; },
             [&](int, int k) {
               dual = dmax(dual, dabs(-yd_[k] - vl_[k] + vu_[k]));
               comp = dmax(comp, dabs((s_[k] - dl_[k]) * vl_[k] - mu_));
@@ -3867,11 +3931,11 @@ struct ObcaSolver {
     const gd* zL = A(L.zL); const gd* zU = A(L.zU); const gd* vL = A(L.vL); const gd* vU = A(L.vU);
     {
       double x_[SW_U], xl_[SW_U], xu_[SW_U];
-      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; },
+      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = ubx(q) ? (double)xU[q] : HTP_INF; },
             [&](int q, int k) {
               const bool hl = finite_(xl_[k]), hu = finite_(xu_[k]);
-              if (hl) { const double v = safe_slack(x_[k] - xl_[k], zL[q], xl_[k], mu_); if (v <= 0) bad = 1; else lg += log(v); if (!hu) lin += v; }
-              if (hu) { const double v = safe_slack(xu_[k] - x_[k], zU[q], xu_[k], mu_); if (v <= 0) bad = 1; else lg += log(v); if (!hl) lin += v; }
+              if (hl) { const double v = safe_slack(x_[k] - xl_[k], zL[q], xl_[k], mu_); if (v <= 0) bad = 1; else lg += sm::log(v); if (!hu) lin += v; }
+              if (hu) { const double v = safe_slack(xu_[k] - x_[k], zU[q], xu_[k], mu_); if (v <= 0) bad = 1; else lg += sm::log(v); if (!hl) lin += v; }
             });
     }
     double fobj = 0.0;
@@ -3889,7 +3953,7 @@ struct ObcaSolver {
         sweep(nR, [&](int j, int k) { v_[k] = Rv[j]; },
               [&](int, int k) {
                 const double v = v_[k];
-                if (v <= 0) bad = 1; else lg += log(v);
+                if (v <= 0) bad = 1; else lg += sm::log(v);
                 lin += v;
                 sr += v;
               });
@@ -3898,13 +3962,13 @@ struct ObcaSolver {
     }
     {
       double s_[SW_U], dl_[SW_U], du_[SW_U];
-      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = dU[r]; },
+      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = ubs(r) ? (double)dU[r] : HTP_INF; },
             [&](int r, int k) {
               const bool hu = finite_(du_[k]);
               const double v = safe_slack(s_[k] - dl_[k], vL[r], dl_[k], mu_);
-              if (v <= 0) bad = 1; else lg += log(v);
+              if (v <= 0) bad = 1; else lg += sm::log(v);
               if (!hu) lin += v;
-              if (hu) { const double w = safe_slack(du_[k] - s_[k], vU[r], du_[k], mu_); if (w <= 0) bad = 1; else lg += log(w); }
+              if (hu) { const double w = safe_slack(du_[k] - s_[k], vU[r], du_[k], mu_); if (w <= 0) bad = 1; else lg += sm::log(w); }
             });
     }
     bad = c.isum(bad);
@@ -3949,7 +4013,7 @@ struct ObcaSolver {
     const double kd = o.kappa_d * mu_;
     {
       double x_[SW_U], xl_[SW_U], xu_[SW_U], g_[SW_U];
-      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; g_[k] = gf[q]; },
+      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = ubx(q) ? (double)xU[q] : HTP_INF; g_[k] = gf[q]; },
             [&](int q, int k) {
               const bool hl = finite_(xl_[k]), hu = finite_(xu_[k]);
               double g = g_[k];
@@ -3962,7 +4026,7 @@ struct ObcaSolver {
     }
     {
       double s_[SW_U], dl_[SW_U], du_[SW_U];
-      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = dU[r]; },
+      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = ubs(r) ? (double)dU[r] : HTP_INF; },
             [&](int r, int k) {
               const bool hu = finite_(du_[k]);
               double g = -mu_ / (s_[k] - dl_[k]);
@@ -3983,7 +4047,7 @@ struct ObcaSolver {
     double a = 1.0;
     {
       double x_[SW_U], xl_[SW_U], xu_[SW_U], d_[SW_U];
-      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; d_[k] = dx[q]; },
+      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = ubx(q) ? (double)xU[q] : HTP_INF; d_[k] = dx[q]; },
             [&](int, int k) {
               if (finite_(xl_[k]) && d_[k] < 0) a = dmin(a, -tau * (x_[k] - xl_[k]) / d_[k]);
               if (finite_(xu_[k]) && -d_[k] < 0) a = dmin(a, -tau * (xu_[k] - x_[k]) / (-d_[k]));
@@ -3991,7 +4055,7 @@ struct ObcaSolver {
     }
     {
       double s_[SW_U], dl_[SW_U], du_[SW_U], d_[SW_U];
-      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = dU[r]; d_[k] = ds[r]; },
+      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = ubs(r) ? (double)dU[r] : HTP_INF; d_[k] = ds[r]; },
             [&](int, int k) {
               if (d_[k] < 0) a = dmin(a, -tau * (s_[k] - dl_[k]) / d_[k]);
               if (finite_(du_[k]) && -d_[k] < 0) a = dmin(a, -tau * (du_[k] - s_[k]) / (-d_[k]));
@@ -4016,7 +4080,7 @@ struct ObcaSolver {
     double a = 1.0;
     {
       double x_[SW_U], xl_[SW_U], xu_[SW_U], zl_[SW_U], zu_[SW_U], d_[SW_U];
-      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; zl_[k] = zL[q]; zu_[k] = zU[q]; d_[k] = dx[q]; },
+      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; xl_[k] = xL[q]; xu_[k] = ubx(q) ? (double)xU[q] : HTP_INF; zl_[k] = zL[q]; zu_[k] = ubx(q) ? (double)zU[q] : 0.0; d_[k] = dx[q]; },
             [&](int q, int k) {
               double t = 0.0, u = 0.0;
               if (finite_(xl_[k])) { const double sl = x_[k] - xl_[k]; t = (mu - zl_[k] * sl - zl_[k] * d_[k]) / sl; if (t < 0) a = dmin(a, -tau * zl_[k] / t); }
@@ -4027,7 +4091,7 @@ struct ObcaSolver {
     }
     {
       double s_[SW_U], dl_[SW_U], du_[SW_U], vl_[SW_U], vu_[SW_U], d_[SW_U];
-      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = dU[r]; vl_[k] = vL[r]; vu_[k] = vU[r]; d_[k] = ds[r]; },
+      sweep(D.md, [&](int r, int k) { s_[k] = s[r]; dl_[k] = dL[r]; du_[k] = ubs(r) ? (double)dU[r] : HTP_INF; vl_[k] = vL[r]; vu_[k] = ubs(r) ? (double)vU[r] : 0.0; d_[k] = ds[r]; },
             [&](int r, int k) {
               const double sl = s_[k] - dl_[k];
               const double t = (mu - vl_[k] * sl - vl_[k] * d_[k]) / sl;
@@ -4079,7 +4143,7 @@ struct ObcaSolver {
       printf("[dbg] factor dw=%g dc=%g neg=%d need=%d zero=%d\n", dw, dc, neg, need, zero);
 #endif
       if (neg == need && zero == 0) return true;
-      if (zero > 0 && dc == 0.0) { dc = o.dc_bar * pow(mu, o.kappa_c); continue; }
+      if (zero > 0 && dc == 0.0) { dc = o.dc_bar * sm::pow(mu, o.kappa_c); continue; }
       if (dw == 0.0) dw = (dw_last == 0.0) ? o.dw0 : dmax(o.dw_min, o.kw_minus * dw_last);
       else dw = ((dw_last == 0.0 || 1e5 * dw_last < dw) ? o.kw_plus_bar : o.kw_plus) * dw;
       if (dw > o.dw_max) return false;
@@ -4143,7 +4207,7 @@ struct ObcaSolver {
     return true;
   }
   HTP_HD HTP_FI bool is_ftype(double th, double gbd, double a) const {
-    return gbd < 0 && a * pow(-gbd, o.s_phi) > o.delta * pow(th, o.s_theta);
+    return gbd < 0 && a * sm::pow(-gbd, o.s_phi) > o.delta * sm::pow(th, o.s_theta);
   }
   HTP_HD HTP_FI bool armijo(double ph, double gbd, double a, double ph_t) const {
     return cmp_le(ph_t - ph, o.eta_phi * a * gbd, ph);
@@ -4393,8 +4457,8 @@ struct ObcaSolver {
     const double ks = o.kappa_sigma;
     {
       double x_[SW_U], d_[SW_U], xl_[SW_U], xu_[SW_U], zl_[SW_U], zu_[SW_U], dzl_[SW_U], dzu_[SW_U];
-      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; d_[k] = dx[q]; xl_[k] = xL[q]; xu_[k] = xU[q]; zl_[k] = zL[q];
-                                      zu_[k] = zU[q]; dzl_[k] = dzL[q]; dzu_[k] = dzU[q]; },
+      sweep(D.n, [&](int q, int k) { x_[k] = x[q]; d_[k] = dx[q]; xl_[k] = xL[q]; xu_[k] = ubx(q) ? (double)xU[q] : HTP_INF; zl_[k] = zL[q];
+                                      zu_[k] = ubx(q) ? (double)zU[q] : 0.0; dzl_[k] = dzL[q]; dzu_[k] = ubx(q) ? (double)dzU[q] : 0.0; },
             [&](int q, int k) {
               const double xn = x_[k] + a_primal * d_[k];
               x[q] = xn;
@@ -4415,7 +4479,7 @@ struct ObcaSolver {
     {
       double s_[SW_U], d_[SW_U], y_[SW_U], dy_[SW_U], vl_[SW_U], dvl_[SW_U], dl_[SW_U], vu_[SW_U], dvu_[SW_U], du_[SW_U];
       sweep(D.md, [&](int r, int k) { s_[k] = s[r]; d_[k] = ds[r]; y_[k] = yd[r]; dy_[k] = dyd[r]; vl_[k] = vL[r];
-                                       dvl_[k] = dvL[r]; dl_[k] = dL[r]; vu_[k] = vU[r]; dvu_[k] = dvU[r]; du_[k] = dU[r]; },
+                                       dvl_[k] = dvL[r]; dl_[k] = dL[r]; vu_[k] = ubs(r) ? (double)vU[r] : 0.0; dvu_[k] = ubs(r) ? (double)dvU[r] : 0.0; du_[k] = ubs(r) ? (double)dU[r] : HTP_INF; },
             [&](int r, int k) {
               const double sn = s_[k] + a_primal * d_[k];
               s[r] = sn;
@@ -4549,7 +4613,7 @@ struct ObcaSolver {
       alpha_min = o.gamma_theta;
       if (gbd < 0) {
         alpha_min = dmin(o.gamma_theta, o.gamma_phi * th / (-gbd));
-        if (th <= theta_min) alpha_min = dmin(alpha_min, o.delta * pow(th, o.s_theta) / pow(-gbd, o.s_phi));
+        if (th <= theta_min) alpha_min = dmin(alpha_min, o.delta * sm::pow(th, o.s_theta) / sm::pow(-gbd, o.s_phi));
       }
       alpha_min *= o.alpha_min_frac;
     }
@@ -4922,7 +4986,7 @@ struct ObcaSolver {
         Err eb = first ? emu : errors(gl, mu);
         const double berr = dmax(dmax(eb.dual / eb.s_d, eb.prim_b), eb.comp / eb.s_c);
         if (berr > o.kappa_eps * mu && !ls_.tiny_flag) break;
-        const double nm = dmax(o.tol / 10.0, dmin(o.kappa_mu * mu, pow(mu, o.theta_mu)));
+        const double nm = dmax(o.tol / 10.0, dmin(o.kappa_mu * mu, sm::pow(mu, o.theta_mu)));
         if (nm == mu) { if (ls_.tiny_flag) stop_tiny = true; break; }
         mu = nm;
         tau = dmax(o.tau_min, 1.0 - mu);

@@ -466,16 +466,65 @@ int htp_orchard_chain_device(htp_ctx* ctx, const htp_chain_batch* in, void* stre
 double htp_chain_last_ms(htp_ctx* ctx);
 
 
+/* ---------------------------------------------------------------------------
+ * The notebook planner chain on the device (R/path_planner/headland_path_planning.py:124-255, the planner of
+ * R/test/obca.ipynb cells 9-15): for each problem, the Y-type parking search (htp_ypark_search_batch_device)
+ * fixes the intermediate pose; the heuristic lowering (csrc/ychain_core.h: get_topology_waypoints, the
+ * ReferenceLineHeuristic guide path, segment lanes and search lengths) writes the hybrid A* inputs of that
+ * problem into reserved slots of the search's pools; the hybrid A* search (htp_hastar_search_batch_device) runs
+ * from the start to the intermediate pose; its path and the parking manoeuvre are joined and turned into the
+ * init guess (get_init_ref_path, refpath_core.h) and resampled to N rows (the OBCA solve's traj input).
+ * Everything stays in HBM; four launches on `stream`.  Reserved hybrid A* slots of problem b: polygon ids
+ * [lane_poly0 + b * HTP_YC_POLY_STRIDE, + HTP_YC_POLY_STRIDE) (the last one spans the unused vertices),
+ * vertices [lane_vert0 + b * HTP_YC_VERT_STRIDE, ...), guide rows [guide0 + b * guide_stride, ...); the host
+ * sets hastar.poly_off at every problem's first slot id (and at lane_poly0 + batch * HTP_YC_POLY_STRIDE), the
+ * device writes the rest, hastar.params[b] GX..GYAW and hastar.desc[b] LANE0..GUIDE1. */
+#define HTP_YC_MAXWP 10
+#define HTP_YC_POLY_STRIDE HTP_YC_MAXWP
+#define HTP_YC_VERT_STRIDE ((HTP_YC_MAXWP - 1) * 80)
+typedef struct {
+  int32_t batch, N;
+  htp_ypark_batch ypark;            /* device arrays */
+  htp_ypark_result ypark_out;       /* device arrays (path: [batch][ypark.cap_path][5]) */
+  htp_hastar_batch hastar;          /* device pools; the lane / guide slots and GX..GYAW, LANE0..GUIDE1 are written */
+  htp_hastar_result hastar_out;     /* device arrays (paths: [batch][hastar.cap_path]) */
+  const double* rows;               /* [batch][max_rows][4]: near x, near y, far x, far y of every tree row */
+  const int32_t* nrows;             /* [batch] */
+  const double* eps;                /* [batch][max_rows]: check_side_of_a_point's uniform(-0.5, 0.5) draws */
+  const double* start;              /* [batch][3] the search start pose */
+  int32_t max_rows;
+  double drive_row_offset;          /* headland_planner_y_type_park's drive_row_offset */
+  int32_t lane_poly0, lane_vert0, guide0, guide_stride;
+  const double* rp_params;          /* [batch][3] WHEEL_BASE, desired_v, ds (get_init_ref_path) */
+  int32_t cap_rows;                 /* init-guess rows per problem */
+  double* ref;                      /* [batch][cap_rows][5] init guess out (get_init_ref_path rows) */
+  int32_t* n_ref;                   /* [batch] */
+  double* traj;                     /* [batch][N][5] the init guess resampled to N rows (OBCA traj) */
+  int32_t* status;                  /* [batch]: 0, or 16 * stage + that stage's status (1 Y-park, 2 lowering,
+                                       3 hybrid A*, 4 init guess) */
+} htp_ychain_batch;
+int htp_ypark_hastar_chain_device(htp_ctx* ctx, const htp_ychain_batch* in, void* stream);
+/* Per-stage kernel times (ms) of the last chain: Y-park, lowering, hybrid A*, init guess + resample. */
+int htp_ychain_last_ms(htp_ctx* ctx, double* ms4);
+
 /* ---- correctly rounded libm of the planner cores (csrc/htp_libm.h) ----------------------------------------
  * Replaces nothing in the reference: the reference's planners call CPython's math module / numpy (glibc, or
  * numpy's SIMD kernels), whose last bits differ between platforms.  Every device planner kernel and every host
  * build of the same cores evaluates sin, cos, tan, atan, atan2, asin, acos, hypot and pow with this one
  * correctly rounded implementation, so integer outputs that hang on the last bit (a spline piece's sample
  * count, R/path_planner/utils/cubic_spline.py:102) are identical on the GPU and on the host.
- * fn: 0 sin, 1 cos, 2 tan, 3 atan, 4 atan2(x[i], y[i]), 5 asin, 6 acos, 7 hypot(x[i], y[i]), 8 pow(x[i], y[i]).
+ * fn: 0 sin, 1 cos, 2 tan, 3 atan, 4 atan2(x[i], y[i]), 5 asin, 6 acos, 7 hypot(x[i], y[i]), 8 pow(x[i], y[i]), 9 log
+ * (the solver's barrier terms).
  * x, y, out: device arrays of n doubles (y only for the two-argument functions). */
 int htp_libm_batch_device(htp_ctx* ctx, int32_t fn, const double* x, const double* y, double* out, int64_t n,
                           void* stream);
+
+/* The fp64 matrix-core op of the solver's Riccati recursion (v_mfma_f64_16x16x4f64) on n caller tiles:
+ * D[t] = A[t] (16x4, row-major) * B[t] (4x16, row-major) + C[t] (16x16, row-major), device arrays.  A
+ * diagnostic surface with no reference counterpart: it pins the host model of the op's rounding that the
+ * bit-exact host emulation of the device solver uses (tests/test_gpu_mfma_model.py). */
+int htp_mfma_f64_probe(htp_ctx* ctx, const double* A, const double* B, const double* C, double* D, int64_t n,
+                       void* stream);
 
 #ifdef __cplusplus
 }

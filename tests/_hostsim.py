@@ -87,6 +87,56 @@ def solve(insts, options=None):
     return res
 
 
+ESO = os.path.join(ROOT, "build", "libhtp_emusim.so")
+CLANG = "/opt/rocm/lib/llvm/bin/clang++"
+
+
+def build_emusim():
+    """The bit-exact host emulation of the device solver (csrc/htp_emusim.cpp, emu_wave.h): clang with the
+    device build's contraction (fused only within an expression) and FMA; the device's wave-reduction and
+    matrix-core order.  TEST-ONLY."""
+    os.makedirs(os.path.dirname(ESO), exist_ok=True)
+    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(ROOT, "include", "htp.h")]
+    if not (os.path.exists(ESO) and os.path.getmtime(ESO) >= max(os.path.getmtime(s) for s in srcs)):
+        subprocess.check_call([CLANG, "-O2", "-std=c++20", "-ffp-contract=on", "-mfma", "-shared", "-fPIC", "-o", ESO,
+                               os.path.join(CSRC, "htp_emusim.cpp"), "-lpthread"])
+    L = ctypes.CDLL(ESO)
+    L.htp_emusim_obca_solve.argtypes = [ctypes.POINTER(_native.ObcaBatch), ctypes.POINTER(_native.ObcaResult),
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    L.htp_emusim_obca_solve.restype = ctypes.c_int
+    L.htp_emusim_obca_points_solve.argtypes = [ctypes.POINTER(_native.ObcaPointsBatch),
+                                               ctypes.POINTER(_native.ObcaResult), ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_int]
+    L.htp_emusim_obca_points_solve.restype = ctypes.c_int
+    return L
+
+
+def _opts(options):
+    opts = dict(options or {})
+    names = (ctypes.c_char_p * max(1, len(opts)))(*[k.encode() for k in opts])
+    vals = (ctypes.c_double * max(1, len(opts)))(*[float(v) for v in opts.values()])
+    return names, vals, len(opts)
+
+
+def solve_emusim(insts, options=None):
+    """OBCA problems through the device emulation -> HostResults (the device's doubles, bit for bit)."""
+    L = build_emusim()
+    pk = _native.PackedBatch(insts)
+    res = _native.HostResults(pk.batch, pk.n_var)
+    b, r = pk.struct(), res.struct()
+    assert L.htp_emusim_obca_solve(ctypes.byref(b), ctypes.byref(r), *_opts(options)) == 0
+    return res
+
+
+def solve_points_emusim(insts, options=None):
+    L = build_emusim()
+    pk = _native.PointsPackedBatch(insts)
+    res = _native.HostResults(pk.batch, pk.n_var)
+    b, r = pk.struct(), res.struct()
+    assert L.htp_emusim_obca_points_solve(ctypes.byref(b), ctypes.byref(r), *_opts(options)) == 0
+    return res
+
+
 def build_threadsim():
     """64-thread wavefront simulation (std::barrier per sync) of the same core."""
     os.makedirs(os.path.dirname(TSO), exist_ok=True)

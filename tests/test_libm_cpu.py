@@ -13,7 +13,7 @@ from headland_trajectory_planning_amd import _native
 
 MP = {"sin": mpmath.sin, "cos": mpmath.cos, "tan": mpmath.tan, "atan": mpmath.atan, "atan2": mpmath.atan2,
       "asin": mpmath.asin, "acos": mpmath.acos, "hypot": lambda a, b: mpmath.sqrt(a * a + b * b),
-      "pow": lambda a, b: a ** b}
+      "pow": lambda a, b: a ** b, "log": mpmath.log}
 
 
 def _args(name, rng, n):
@@ -27,6 +27,8 @@ def _args(name, rng, n):
     if name in ("atan2", "hypot"):
         return (np.concatenate([rng.uniform(-10, 10, n), lg(1e-150, 1e150)]),
                 np.concatenate([rng.uniform(-10, 10, n), lg(1e-150, 1e150)]))
+    if name == "log":
+        return np.abs(np.concatenate([rng.uniform(0, 100, n), lg(1e-320, 1e300), 1.0 + lg(1e-17, 1e-3)])), None
     x = np.abs(np.concatenate([rng.uniform(0, 100, n), lg(1e-100, 1e100), rng.uniform(0.1, 10, n)]))
     return x, np.concatenate([np.full(n, 1.5), np.full(n, 2.0), rng.uniform(-20, 20, n)])
 
@@ -52,14 +54,15 @@ def _same(a, b):
 def test_special_values():
     inf, nan = math.inf, math.nan
     S = [0.0, -0.0, 1.0, -1.0, 0.5, -2.0, inf, -inf, nan, 5e-324, 1e300, -1e300, math.pi, 1e22]
-    unary = {"sin": math.sin, "cos": math.cos, "tan": math.tan, "atan": math.atan, "asin": math.asin, "acos": math.acos}
+    unary = {"sin": math.sin, "cos": math.cos, "tan": math.tan, "atan": math.atan, "asin": math.asin, "acos": math.acos,
+             "log": math.log}
     for name, f in unary.items():
         got = _native.cpu_libm(name, np.array(S))
         for v, g in zip(S, got):
             try:
                 ref = f(v)
             except ValueError:
-                ref = nan
+                ref = -inf if (name == "log" and v == 0.0) else nan
             if name in ("sin", "cos", "tan") and abs(v) >= 1e22:   # glibc is not correctly rounded everywhere there
                 ref = float(getattr(mpmath, name)(mpmath.mpf(v))) if math.isfinite(v) else ref
             assert _same(g, ref), (name, v, g, ref)

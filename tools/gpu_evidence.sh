@@ -9,6 +9,7 @@
 #     kernels  hybrid A* and point-formulation throughput
 #     ws2      2-rank rehearsal of the multi-GPU bench on one GPU (gloo: RCCL refuses two ranks on one device)
 #     pytest:FILE[,FILE...]   only these GPU test files (tests/FILE)
+#     pytestk:FILE[,...]      the same, every test (no -x, output shown) and the script goes on after test failures
 #     benchC / benchE / benchD20   config C at 6 steps, config E, config D at 20 steps
 #     pmcC / pmcE    PMC passes for configs C / E only
 #     stall    the three SQ stall passes (tools/gpu_stall.sh) on config D
@@ -50,8 +51,14 @@ for S in "$@"; do
              run points 300 python -u tools/bench_points.py ;;
     ws2) HTP_DIST_BACKEND=gloo run ws2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
            --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --batch 4096 --steps 2 --waves 512 --gen-procs 8 ;;
+    pytestk:*) files=$(echo "${S#pytestk:}" | tr ',' ' ' | sed 's|\([^ ]*\)|tests/\1|g')
+               timeout -k 10 900 python -u -m pytest $files -m gpu -v -s --timeout 600 --timeout-method thread \
+                 > gpurun_out/${T}_pytestk.out 2> gpurun_out/${T}_pytestk.err
+               rc=$?; echo "pytestk rc=$rc"; grep -E "PASS|FAIL|ERROR|SKIP|model\]" gpurun_out/${T}_pytestk.out | cut -c1-300
+               [ $rc -le 1 ] || exit $rc ;;   # test failures (1) go on; a crash, abort or time limit stops
     pytest:*) files=$(echo "${S#pytest:}" | tr ',' ' ' | sed 's|\([^ ]*\)|tests/\1|g')
               run pytest_sel 900 python -u -m pytest $files -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    ychain) run ychain 600 python -u bench.py --e2e --planner ypark_hastar --steps 3 --warmup 1 ;;
     benchC) run benchC 600 python -u bench.py --config C --steps 6 --no-cpu-baseline ;;
     benchE) run benchE 900 python -u bench.py --config E --steps 1 --warmup 0 --no-cpu-baseline ;;
     benchD20) run benchD20 900 python -u bench.py --steps 20 --no-cpu-baseline ;;

@@ -66,6 +66,7 @@ def main():
     per_it_raw = (fkb * 1024) / it_f + (wkb * 1024) / it_w
     traffic = {
         "workload": cfg, "batch": bl_f["config"]["global_batch"], "solver_sha": sha, "kernel": meta.get("kernel"),
+        "binary": bl_f.get("binary"),
         "resources": {k: meta.get(k) for k in ("grid", "scratch", "vgpr", "agpr", "sgpr", "lds")},
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (tools/gpu_pmc.sh), one "
                   "persistent launch each; counters in kB",
