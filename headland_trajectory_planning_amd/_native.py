@@ -190,13 +190,15 @@ def _declare(lib):
     lib.htp_libm_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int32] + [ctypes.c_void_p] * 3 + \
         [ctypes.c_int64, ctypes.c_void_p]
     lib.htp_libm_batch_device.restype = ctypes.c_int
-    lib.htp_mfma_f64_probe.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_void_p]
-    lib.htp_mfma_f64_probe.restype = ctypes.c_int
+    if hasattr(lib, "htp_mfma_f64_probe"):   # absent from libraries built before it (A/B variants of old kernels)
+        lib.htp_mfma_f64_probe.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_void_p]
+        lib.htp_mfma_f64_probe.restype = ctypes.c_int
     return lib
 
 
 # correctly rounded libm of the planner cores (csrc/htp_libm.h): function ids of htp_libm_batch_device
-LIBM_FN = {"sin": 0, "cos": 1, "tan": 2, "atan": 3, "atan2": 4, "asin": 5, "acos": 6, "hypot": 7, "pow": 8, "log": 9}
+LIBM_FN = {"sin": 0, "cos": 1, "tan": 2, "atan": 3, "atan2": 4, "asin": 5, "acos": 6, "hypot": 7, "pow": 8, "log": 9,
+           "fast_log": 10, "fast_sin": 11, "fast_cos": 12, "fast_tan": 13}
 LIBM_BINARY = {"atan2", "hypot", "pow"}
 CPU_LIB_PATH = os.path.join(HERE, "libhtp_cpu.so")
 _CPU_LIB = None

@@ -17,24 +17,26 @@
 #include <cmath>
 
 #include "htp_common.h"
+#include "htp_fastm.h"
 #include "htp_libm.h"
 
-// The solver's transcendental functions (dynamics sin / cos / tan, barrier log, IPOPT's pow updates).  With
-// HTP_SOLVER_CRLIBM (default) they are the correctly rounded htp_libm.h functions on the device and on every
-// host build, so the device solve is reproducible bit for bit on the host (the emulation of csrc/emu_wave.h,
-// tests/test_gpu_emulation.py); 0 takes the platform's (ocml on the device).
-#ifndef HTP_SOLVER_CRLIBM
-#define HTP_SOLVER_CRLIBM 1
+// The solver's transcendental functions.  With HTP_SOLVER_DETLIBM (default) the same doubles on the device and on
+// every host build, so the device solve is reproduced on the host bit for bit (emu_wave.h,
+// tests/test_gpu_emulation.py): the hot ones (dynamics sin / cos / tan, the barrier's log) from htp_fastm.h
+// (explicit FMA, <= 2 ulp), IPOPT's few pow updates per iteration correctly rounded (htp_libm.h).  0 takes the
+// platform's (ocml on the device).
+#ifndef HTP_SOLVER_DETLIBM
+#define HTP_SOLVER_DETLIBM 1
 #endif
 namespace htp {
 namespace sm {
-#if HTP_SOLVER_CRLIBM
-using hm::cos;
-using hm::log;
+#if HTP_SOLVER_DETLIBM
+using fm::cos;
+using fm::log;
+using fm::sin;
+using fm::sincos;
+using fm::tan;
 using hm::pow;
-using hm::sin;
-using hm::sincos;
-using hm::tan;
 #else
 HTP_HD inline double sin(double x) { return ::sin(x); }
 HTP_HD inline double cos(double x) { return ::cos(x); }

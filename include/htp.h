@@ -513,8 +513,8 @@ int htp_ychain_last_ms(htp_ctx* ctx, double* ms4);
  * build of the same cores evaluates sin, cos, tan, atan, atan2, asin, acos, hypot and pow with this one
  * correctly rounded implementation, so integer outputs that hang on the last bit (a spline piece's sample
  * count, R/path_planner/utils/cubic_spline.py:102) are identical on the GPU and on the host.
- * fn: 0 sin, 1 cos, 2 tan, 3 atan, 4 atan2(x[i], y[i]), 5 asin, 6 acos, 7 hypot(x[i], y[i]), 8 pow(x[i], y[i]), 9 log
- * (the solver's barrier terms).
+ * fn: 0 sin, 1 cos, 2 tan, 3 atan, 4 atan2(x[i], y[i]), 5 asin, 6 acos, 7 hypot(x[i], y[i]), 8 pow(x[i], y[i]), 9 log; the solver's
+ * fast deterministic functions (htp_fastm.h, <= 2 ulp): 10 log, 11 sin, 12 cos, 13 tan.
  * x, y, out: device arrays of n doubles (y only for the two-argument functions). */
 int htp_libm_batch_device(htp_ctx* ctx, int32_t fn, const double* x, const double* y, double* out, int64_t n,
                           void* stream);

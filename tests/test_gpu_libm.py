@@ -30,9 +30,11 @@ def test_device_equals_host(ctx, name):
     rng = np.random.default_rng(100 + _native.LIBM_FN[name])
     n = 1 << 17
     lg = np.exp(rng.uniform(np.log(1e-12), np.log(1e12), n)) * rng.choice([-1.0, 1.0], n)
-    base = {"sin": 20, "cos": 20, "tan": 1.6, "atan": 5, "atan2": 10, "asin": 1, "acos": 1, "hypot": 10, "pow": 100, "log": 100}[name]
+    base = {"sin": 20, "cos": 20, "tan": 1.6, "atan": 5, "atan2": 10, "asin": 1, "acos": 1, "hypot": 10, "pow": 100,
+            "log": 100, "fast_log": 100, "fast_sin": 20,
+            "fast_cos": 20, "fast_tan": 1.6}[name]
     x = np.concatenate([rng.uniform(-base, base, n), lg])
-    if name == "log":
+    if name in ("log", "fast_log"):
         x = np.abs(x)
     if name in ("asin", "acos"):
         x = np.clip(x, -1.0, 1.0) * rng.uniform(0.0, 1.0, 2 * n) ** 0.1

@@ -33,7 +33,33 @@ def _args(name, rng, n):
     return x, np.concatenate([np.full(n, 1.5), np.full(n, 2.0), rng.uniform(-20, 20, n)])
 
 
-@pytest.mark.parametrize("name", list(_native.LIBM_FN))
+CR = [k for k in _native.LIBM_FN if not k.startswith("fast_")]
+FAST = [k for k in _native.LIBM_FN if k.startswith("fast_")]
+
+
+@pytest.mark.parametrize("name", FAST)
+def test_fast_functions_within_two_ulp(name):
+    """The solver's hot-loop functions (csrc/htp_fastm.h): not correctly rounded, but within 2 ulp (tan: 3), and the same
+    doubles on the device (tests/test_gpu_libm.py)."""
+    mpmath.mp.prec = 200
+    base = name[5:]
+    rng = np.random.default_rng(70 + _native.LIBM_FN[name])
+    if base == "log":
+        x = np.abs(np.concatenate([rng.uniform(0, 100, 3000), np.exp(rng.uniform(-700, 700, 3000)),
+                                   1.0 + rng.uniform(-1e-3, 1e-3, 2000), np.exp(rng.uniform(-740, -708, 200))]))
+    else:
+        x = np.concatenate([rng.uniform(-7, 7, 4000), rng.uniform(-1, 1, 2000) * 10.0 ** rng.integers(-10, 5, 2000)])
+        if base == "tan":
+            x = x[np.abs(np.cos(x)) > 1e-3]
+    got = _native.cpu_libm(name, x)
+    worst = 0.0
+    for v, g in zip(x, got):
+        ref = getattr(mpmath, base)(mpmath.mpf(float(v)))
+        worst = max(worst, float(abs(mpmath.mpf(float(g)) - ref) / mpmath.mpf(math.ulp(float(ref)))))
+    assert worst <= (3.0 if base == "tan" else 2.0), (name, worst)
+
+
+@pytest.mark.parametrize("name", CR)
 def test_correctly_rounded(name):
     mpmath.mp.prec = 300
     rng = np.random.default_rng(7 + _native.LIBM_FN[name])
