@@ -69,6 +69,11 @@ HTP_HD inline void sincos(double x, double& s, double& c) {
 #endif
 // loads in flight per lane in sweep(): 8 and 12 give the fewest cycles per iteration, 4 is 4 % and 2 is 14 % slower,
 // 16 is slower again (profiles/r03t_ab_sweep_unroll.txt, r03u_ab_sweep_unroll.txt; results bit-identical)
+// Riccati factor: stop at the first non-positive-definite pivot (the inertia is then decided; 1) or run every stage
+// (0, the round-3 kernel) -- bit-identical results, fewer cycles in inertia-correction trials
+#ifndef HTP_RIC_EARLY_EXIT
+#define HTP_RIC_EARLY_EXIT 1
+#endif
 #ifndef HTP_SWEEP_U
 #define HTP_SWEEP_U 8
 #endif
@@ -2557,6 +2562,7 @@ struct ObcaSolver {
       c.sync();
       if (ric_relax && !relax_P(Pc, i, dc, c.lds + 240, trec(i))) ++bad;
       HTP_PROF(5);
+      if (HTP_RIC_EARLY_EXIT && bad) break;   // wrong inertia is decided (the caller rejects or re-factors)
     }
     return bad;
   }
@@ -2696,6 +2702,10 @@ struct ObcaSolver {
       fcur[0] = fnxt[0];
       fcur[1] = fnxt[1];
       HTP_PROF(5);
+      // A non-positive-definite pivot decides the inertia (wrong: factor_ic perturbs and re-factors; the point
+      // formulation's block LDL^T re-derives it from the assembled blocks): the remaining stages are not needed.
+      // Wave-uniform (every lane holds the same pivot test); successful factorizations are unchanged.
+      if (HTP_RIC_EARLY_EXIT && bad) break;
     }
     return bad;
   }

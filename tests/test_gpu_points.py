@@ -52,7 +52,10 @@ WITNESS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "wi
 # Restoration cycles the reference algorithm does not determine at rounding level: the oracle itself, with the
 # structured elimination order of the same KKT systems (StructuredPointKKT), ends 3.4 away from its dense-KKT
 # run (177 vs 234 iterations; tests/golden/witness/P19.npz, tests/golden/make_witness.py).  The device must
-# end with the oracle's status at a KKT point of the same NLP.  Every other restoration case: state parity.
+# end with the oracle's status at a KKT point of the same NLP, and its run must be the host emulation's of the
+# device summation order bit for bit (tests/golden/emulation/P19.npz, make_emulation.py).  Every other
+# restoration case: state parity.
+EMULATION = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "emulation")
 CHAOTIC = {19: "P19"}
 
 
@@ -74,6 +77,9 @@ def test_gpu_matches_oracle_quads(ctx):
             w = np.load(os.path.join(WITNESS, CHAOTIC[k] + ".npz"))
             assert int(w["status_a"]) == ref["status"] and int(w["iters_a"]) == ref["iters"]   # the fixture is this run
             assert np.max(np.abs(w["states_a"] - w["states_b"])) > 1e-4                        # the witness holds
+            e = np.load(os.path.join(EMULATION, CHAOTIC[k] + ".npz"))                          # the device's order
+            assert int(e["status"]) == g.status[k] and int(e["iters"]) == g.iterations[k]
+            assert np.array_equal(e["x"].view(np.int64), g.x[k].view(np.int64))
             ok = _feasible(inst, g.x[k]) and _stationarity(PointNLP(inst), g.x[k]) <= 1e-5
         elif ok and g.status[k] in (0, 1):
             ok = err <= 1e-4 and _feasible(inst, g.x[k])

@@ -15,6 +15,7 @@
 #     stall    the three SQ stall passes (tools/gpu_stall.sh) on config D
 #     diag     I-cache / TLB / L2 / L1 passes (tools/gpu_diag.sh) on config D
 #     ab:CFG:B:name,name...   A/B of libhtp_<name>.so variants (tools/build_variants.py; "base" = libhtp.so)
+#     slow:CFG:MAXIT:PID,..:name,..  tools/slow_probe.py (per-problem kernel time / factorizations under variants)
 #     counters  rocprofv3 --list-avail (the PMC counter names of this box)
 #     tail      tools/tail_probe.py on config D 32768 (per-problem cycles -> TAG_tail_D.npz for scale_projection.py)
 # Every GPU step has its own time limit; the script stops at the first failure.
@@ -61,6 +62,7 @@ for S in "$@"; do
     ychain) run ychain 600 python -u bench.py --e2e --planner ypark_hastar --steps 3 --warmup 1 ;;
     benchC) run benchC 600 python -u bench.py --config C --steps 6 --no-cpu-baseline ;;
     benchE) run benchE 900 python -u bench.py --config E --steps 1 --warmup 0 --no-cpu-baseline ;;
+    benchE512) run benchE512 900 python -u bench.py --config E --steps 1 --warmup 0 --no-cpu-baseline --waves 512 ;;
     benchD20) run benchD20 900 python -u bench.py --steps 20 --no-cpu-baseline ;;
     pmcC) bash tools/gpu_pmc.sh ${T}C --config C --batch 4096 || exit 1 ;;
     pmcE) bash tools/gpu_pmc.sh ${T}E --config E --batch 1024 || exit 1 ;;
@@ -68,6 +70,8 @@ for S in "$@"; do
     diag) bash tools/gpu_diag.sh ${T}D || exit 1 ;;
     ab:*) IFS=: read -r _ cfg nb names <<< "$S"
           run ab_$cfg 900 python -u tools/ab_phase.py $cfg $nb $(echo $names | tr ',' ' ') ;;
+    slow:*) IFS=: read -r _ cfg mi pids names <<< "$S"
+            run slow_$cfg 600 python -u tools/slow_probe.py $cfg $mi $pids $names ;;
     counters) run counters 120 rocprofv3 --list-avail ;;
     tail) run tailgen 300 python -u bench.py --gen-only --cache /tmp/htp_instcache
           run tail 600 python -u tools/tail_probe.py D 32768 /tmp/htp_instcache gpurun_out/${T}_tail_D.npz ;;
