@@ -37,12 +37,18 @@ using fm::sin;
 using fm::sincos;
 using fm::tan;
 using hm::pow;
+#if HTP_LOG10_PLATFORM
+HTP_HD inline double log10(double x) { return ::log10(x); }
+#else
+HTP_HD inline double log10(double x) { return fm::log(x) * 0.43429448190325182765; }   // the obj_max_inc test
+#endif
 #else
 HTP_HD inline double sin(double x) { return ::sin(x); }
 HTP_HD inline double cos(double x) { return ::cos(x); }
 HTP_HD inline double tan(double x) { return ::tan(x); }
 HTP_HD inline double log(double x) { return ::log(x); }
 HTP_HD inline double pow(double x, double y) { return ::pow(x, y); }
+HTP_HD inline double log10(double x) { return ::log10(x); }
 HTP_HD inline void sincos(double x, double& s, double& c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   ::sincos(x, &s, &c);
@@ -73,6 +79,14 @@ HTP_HD inline void sincos(double x, double& s, double& c) {
 // (0, the round-3 kernel) -- bit-identical results, fewer cycles in inertia-correction trials
 #ifndef HTP_RIC_EARLY_EXIT
 #define HTP_RIC_EARLY_EXIT 1
+#endif
+// factor_ic's inertia scan (see ObcaSolver::ic_scan): 1 on, 0 off (every trial factorization run in full)
+// NaN steps and trial values are evaluation errors (never accepted, never a tiny step): 1; 0 = round-3 behaviour
+#ifndef HTP_NAN_GUARD
+#define HTP_NAN_GUARD 1
+#endif
+#ifndef HTP_IC_SCAN
+#define HTP_IC_SCAN 1
 #endif
 #ifndef HTP_SWEEP_U
 #define HTP_SWEEP_U 8
@@ -128,6 +142,7 @@ struct ProblemIn {
 HTP_HD HTP_FI inline double sq(double a) { return a * a; }
 HTP_HD inline bool finite_(double a) { return a > -1e300 && a < 1e300; }
 HTP_HD inline double dmax(double a, double b) { return a > b ? a : b; }
+HTP_HD inline double nmax(double a, double b) { return (b > a || b != b) ? b : a; }   // NaN-sticky max
 HTP_HD inline double dmin(double a, double b) { return a < b ? a : b; }
 HTP_HD inline double dabs(double a) { return a < 0 ? -a : a; }
 
@@ -415,6 +430,12 @@ struct ObcaSolver {
   double theta_min, theta_max;
   int n_factor;
   bool use_ric = false;
+  // Inertia scan (factor_ic, HTP_IC_SCAN): while a trial factorization's local sweep has its blocks loaded, a
+  // block with the wrong inertia is re-factored at the next trial values of delta_w until it has the right one;
+  // ic_skip = how many more delta_w increments factor_ic may take at once (every skipped trial is known to fail
+  // on that block, with no zero pivot) -- the same delta_w sequence and the same accepted factorization.
+  bool ic_scan = false;
+  int ic_skip = 0;
   // restoration phase (oracle/ipm.py RestoProblem): the iterate is [x, R] with R = [n_c | p_c | n_d | p_d] >= 0,
   // constraints c(x) + n_c - p_c = 0, d(x) + n_d - p_d - s = 0, objective rho sum R + eta/2 |D_R (x - x_R)|^2
   bool rs = false;
@@ -1337,6 +1358,19 @@ struct ObcaSolver {
   // any pivoted block ran that path for the whole wave -- nearly every trip.  Each block's
   // arithmetic is unchanged, so the results are bit-identical.
   template <int EN, int EM>
+  // inertia of local block p at (dw, dc), exactly as local_factor_sweep decides it (LDL^T, or Bunch-Kaufman when
+  // that needs pivoting)
+  HTP_HD HTP_FI void block_inertia(int p, bool ls, double dw, double dc, int& nb, int& zb) {
+    LocalBlock<EN, EM> B;
+    build_local<EN, EM>(B, p, ls, dw, dc);
+    B.factor();
+    if (!B.piv) { nb = B.neg; zb = B.zero ? 1 : 0; return; }
+    int pn[2];
+    local_pivoted<EN, EM>(p, ls, dw, dc, nullptr, 0, pn);
+    nb = pn[0];
+    zb = pn[1] ? 1 : 0;
+  }
+  template <int EN, int EM>
   HTP_HD HTP_FI void local_factor_sweep(bool ls, double dw, double dc, int& neg, int& zero) {
     if constexpr (PT) {
       local_factor_sweep_pt(ls, dw, dc, neg, zero);
@@ -1349,6 +1383,22 @@ struct ObcaSolver {
       return (col == 0) ? 0 : (col == 1 ? (row == 0 ? 1 : 2) : (row == 0 ? 3 : (row == 1 ? 4 : 5)));
     };
     int npiv = 0;  // wave-uniform
+    // inertia scan (ic_scan): this lane's latest first-right candidate and earliest zero-pivot candidate
+    int sc_pass = 0, sc_zero = 1 << 20;
+    auto scan = [&](int p, int neg_b, int zero_b) {
+      if (neg_b == 2 && !zero_b) return;
+      if (zero_b && dc == 0.0) { sc_zero = 0; return; }   // (the trial's own dc event: no scan needed)
+      double dwj = dw;
+      for (int j = 1; j <= 64; ++j) {
+        dwj = next_dw(dwj);
+        if (!(dwj <= o.dw_max)) { sc_pass = sc_pass > j ? sc_pass : j; return; }
+        int nb_, zb_;
+        block_inertia<EN, EM>(p, ls, dwj, dc, nb_, zb_);
+        if (zb_ && dc == 0.0) { sc_zero = sc_zero < j ? sc_zero : j; return; }
+        if (nb_ == 2 && !zb_) { sc_pass = sc_pass > j ? sc_pass : j; return; }
+      }
+      sc_pass = 64;
+    };
     for (int b0 = 0; b0 < D.P; b0 += c.width) {
       const int p = b0 + c.lane;
       bool piv = false;
@@ -1363,6 +1413,7 @@ struct ObcaSolver {
         if (!piv) {
           neg += B.neg;
           zero |= B.zero;
+          const int nb0 = B.neg, zb0 = B.zero ? 1 : 0;
           // B' K^-1 B = W' D^-1 W with W = L^-1 B: forward substitutions only
           double W[3][NL];
           for (int col = 0; col < 3; ++col) {
@@ -1379,6 +1430,7 @@ struct ObcaSolver {
               S[sidx(row, col)] = acc;
             }
           for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
+          if (ic_scan) scan(p, nb0, zb0);   // after the block is dead (registers)
         }
       }
       int cnt;
@@ -1408,7 +1460,13 @@ struct ObcaSolver {
             S[sidx(row, col)] = acc;
           }
         for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
+        if (ic_scan) scan(p, pn[0], pn[1]);
       }
+    }
+    if (ic_scan) {   // every trial before min(latest first-right, earliest zero) fails without a zero pivot
+      const int pass = (int)c.maxv((double)sc_pass), zr = (int)c.minv((double)sc_zero);
+      const int first = pass < zr ? pass : zr;
+      ic_skip = first > 1 ? first - 1 : 0;
     }
   }
 
@@ -4149,17 +4207,26 @@ struct ObcaSolver {
     const int need = D.mc + D.md;
     for (;;) {
       int neg, zero;
+      ic_scan = HTP_IC_SCAN && !PT && !rs;
+      ic_skip = 0;
       factorize(false, dw, dc, neg, zero);
+      ic_scan = false;
       ++n_factor;
 #ifdef HTP_HOST_DEBUG
-      printf("[dbg] factor dw=%g dc=%g neg=%d need=%d zero=%d\n", dw, dc, neg, need, zero);
+      printf("[dbg] factor dw=%g dc=%g neg=%d need=%d zero=%d skip=%d\n", dw, dc, neg, need, zero, ic_skip);
 #endif
       if (neg == need && zero == 0) return true;
       if (zero > 0 && dc == 0.0) { dc = o.dc_bar * sm::pow(mu, o.kappa_c); continue; }
-      if (dw == 0.0) dw = (dw_last == 0.0) ? o.dw0 : dmax(o.dw_min, o.kw_minus * dw_last);
-      else dw = ((dw_last == 0.0 || 1e5 * dw_last < dw) ? o.kw_plus_bar : o.kw_plus) * dw;
-      if (dw > o.dw_max) return false;
+      for (int k = 0; k <= ic_skip; ++k) {
+        dw = next_dw(dw);
+        if (dw > o.dw_max) return false;
+      }
     }
+  }
+  // IPOPT's next trial delta_w after a factorization with the wrong inertia
+  HTP_HD HTP_FI double next_dw(double dw) const {
+    if (dw == 0.0) return (dw_last == 0.0) ? o.dw0 : dmax(o.dw_min, o.kw_minus * dw_last);
+    return ((dw_last == 0.0 || 1e5 * dw_last < dw) ? o.kw_plus_bar : o.kw_plus) * dw;
   }
 
   // ---------------------------------------------------------- filter / acceptor state
@@ -4226,14 +4293,14 @@ struct ObcaSolver {
   }
   HTP_HD HTP_FI bool acc_to_iterate(double th, double ph, double ph_t, double th_t, bool from_resto) const {
     if (!from_resto && ph_t > ph) {
-      const double basval = dabs(ph) > 10.0 ? log10(dabs(ph)) : 1.0;
-      if (log10(ph_t - ph) > o.obj_max_inc + basval) return false;
+      const double basval = dabs(ph) > 10.0 ? sm::log10(dabs(ph)) : 1.0;
+      if (sm::log10(ph_t - ph) > o.obj_max_inc + basval) return false;
     }
     return cmp_le(th_t, (1 - o.gamma_theta) * th, th) || cmp_le(ph_t - ph, -o.gamma_phi * th, ph);
   }
   // FilterLSAcceptor::CheckAcceptabilityOfTrialPoint against reference (th, ph, gbd)
   HTP_HD HTP_FI bool check_trial(double th, double ph, double gbd, double a_test, double th_t, double ph_t) {
-    if (th_t > theta_max || !(ph_t < 1e300)) return false;
+    if ((HTP_NAN_GUARD ? !(th_t <= theta_max) : th_t > theta_max) || !(ph_t < 1e300)) return false;   // NaN: evaluation error
     bool ok;
     if (a_test > 0 && is_ftype(th, gbd, a_test) && th <= theta_min) ok = armijo(ph, gbd, a_test, ph_t);
     else ok = acc_to_iterate(th, ph, ph_t, th_t, false);
@@ -4540,30 +4607,32 @@ struct ObcaSolver {
     {
       double d_[SW_U], x_[SW_U];
       sweep(D.n, [&](int q, int k) { d_[k] = dx[q]; x_[k] = x[q]; },
-            [&](int, int k) { mx = dmax(mx, dabs(d_[k]) / (1.0 + dabs(x_[k]))); });
+            [&](int, int k) { mx = nmax(mx, dabs(d_[k]) / (1.0 + dabs(x_[k]))); });
       if (rs) {
         const gd* R = A(L.R);
         sweep(nR, [&](int j, int k) { d_[k] = dR[j]; x_[k] = R[j]; },
-              [&](int, int k) { mx = dmax(mx, dabs(d_[k]) / (1.0 + dabs(x_[k]))); });
+              [&](int, int k) { mx = nmax(mx, dabs(d_[k]) / (1.0 + dabs(x_[k]))); });
       }
     }
     {
       double d_[SW_U], s_[SW_U], y_[SW_U], v_[SW_U];
       sweep(D.md, [&](int r, int k) { d_[k] = ds[r]; s_[k] = s[r]; y_[k] = dyd[r]; v_[k] = dd[r]; },
             [&](int, int k) {
-              ms = dmax(ms, dabs(d_[k]) / (1.0 + dabs(s_[k])));
-              my = dmax(my, dabs(y_[k]));
-              pv = dmax(pv, dabs(v_[k] - s_[k]));
+              ms = nmax(ms, dabs(d_[k]) / (1.0 + dabs(s_[k])));
+              my = nmax(my, dabs(y_[k]));
+              pv = nmax(pv, dabs(v_[k] - s_[k]));
             });
     }
     {
       double y_[SW_U], c_[SW_U];
       sweep(D.mc, [&](int r, int k) { y_[k] = dyc[r]; c_[k] = cc[r]; },
             [&](int, int k) {
-              my = dmax(my, dabs(y_[k]));
-              pv = dmax(pv, dabs(c_[k]));
+              my = nmax(my, dabs(y_[k]));
+              pv = nmax(pv, dabs(c_[k]));
             });
     }
+    // a NaN anywhere in the step is not a tiny step (the wave maxima below drop NaN operands)
+    if (HTP_NAN_GUARD && c.isum((mx == mx && ms == ms && my == my && pv == pv) ? 0 : 1) > 0) return false;
     mx = c.maxv(mx); ms = c.maxv(ms); my = c.maxv(my); pv = c.maxv(pv);
     if (mx > o.tiny_step_tol || ms > o.tiny_step_tol) return false;
     if (my >= o.tiny_step_y_tol) return false;
@@ -5032,7 +5101,11 @@ struct ObcaSolver {
       double theta = (theta_cache >= 0.0) ? theta_cache : theta_of(cc, dd, s);
       bool goto_resto = ls_.fallback != 0;
       ls_.fallback = 0;
-      const double gbd = goto_resto ? 0.0 : newton_gbd(dx, ds, dR);
+      double gbd = goto_resto ? 0.0 : newton_gbd(dx, ds, dR);
+      // A step with a NaN / infinite entry (a KKT system solved beyond floating-point range): IPOPT cuts back on
+      // every trial-point evaluation error and so never takes such a step -- its line search fails and the
+      // restoration phase is called, which is where this goes directly.
+      if (HTP_NAN_GUARD && !goto_resto && !(dabs(gbd) < HTP_INF)) { goto_resto = true; gbd = 0.0; }
       copy_arr(A(L.sx), A(L.xt), D.n);  // keep the Newton rhs (x part) for second-order corrections
       double rth = theta, rph = phi, rgbd = gbd;
       if (ls_.in_wd) { rth = ls_.wd_th; rph = ls_.wd_ph; rgbd = ls_.wd_gbd; }

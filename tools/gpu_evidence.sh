@@ -16,6 +16,7 @@
 #     diag     I-cache / TLB / L2 / L1 passes (tools/gpu_diag.sh) on config D
 #     ab:CFG:B:name,name...   A/B of libhtp_<name>.so variants (tools/build_variants.py; "base" = libhtp.so)
 #     slow:CFG:MAXIT:PID,..:name,..  tools/slow_probe.py (per-problem kernel time / factorizations under variants)
+#     fx:NAME,..:variant,..   tools/fixture_probe.py (oracle fixtures under A/B variants)
 #     counters  rocprofv3 --list-avail (the PMC counter names of this box)
 #     tail      tools/tail_probe.py on config D 32768 (per-problem cycles -> TAG_tail_D.npz for scale_projection.py)
 # Every GPU step has its own time limit; the script stops at the first failure.
@@ -72,6 +73,8 @@ for S in "$@"; do
           run ab_$cfg 900 python -u tools/ab_phase.py $cfg $nb $(echo $names | tr ',' ' ') ;;
     slow:*) IFS=: read -r _ cfg mi pids names <<< "$S"
             run slow_$cfg 600 python -u tools/slow_probe.py $cfg $mi $pids $names ;;
+    fx:*) IFS=: read -r _ names vars <<< "$S"
+          run fx 900 python -u tools/fixture_probe.py $names $vars ;;
     counters) run counters 120 rocprofv3 --list-avail ;;
     tail) run tailgen 300 python -u bench.py --gen-only --cache /tmp/htp_instcache
           run tail 600 python -u tools/tail_probe.py D 32768 /tmp/htp_instcache gpurun_out/${T}_tail_D.npz ;;
