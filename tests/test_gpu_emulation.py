@@ -54,7 +54,7 @@ def test_point_formulation_equals_the_emulation(ctx):
     _same(ctx.solve_points(_native.PointsPackedBatch(insts)), H.solve_points_emusim(insts))
 
 
-@pytest.mark.parametrize("name", ["P19", "D347", "E84", "E6", "E12"])
+@pytest.mark.parametrize("name", ["P19", "D347", "E84", "E6", "E12", "E54"])
 def test_divergent_fixtures_equal_the_emulation(ctx, name):
     path = os.path.join(EMU, f"{name}.npz")
     if not os.path.exists(path):
