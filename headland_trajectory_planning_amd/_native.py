@@ -238,7 +238,7 @@ def core_sha():
     """Short hash of the OBCA solver sources (ties profiles/*_traffic.json to a solver version)."""
     import hashlib
     h = hashlib.sha256()
-    for f in ("obca_core.h", "htp_common.h", "htp_obca.hip", "dyn_gen.h", "wave_ctx.h"):
+    for f in ("obca_core.h", "htp_common.h", "htp_obca.hip", "dyn_gen.h", "wave_ctx.h", "htp_fastm.h", "htp_libm.h"):
         with open(os.path.join(HERE, "csrc", f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:12]

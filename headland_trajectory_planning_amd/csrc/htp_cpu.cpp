@@ -56,6 +56,46 @@ extern "C" int htp_cpu_obca_solve_range(const htp_obca_batch* in, htp_obca_resul
   return 0;
 }
 
+// The point formulation (optimizer_points.py) on the host cores: the same core, FORM 1 -- the CPU baseline of
+// tools/bench_points.py.
+extern "C" int htp_cpu_obca_points_solve_range(const htp_obca_points_batch* in, htp_obca_result* out, int64_t first,
+                                               int64_t count, int nthreads) {
+  const char* e = nullptr;
+  if (check_shape_points(in, &e) || first < 0 || first + count > in->batch) return -1;
+  Options o = default_options();
+  o.wall_rate = 1e9;
+  Dims D;
+  make_dims_points(D, in->N, in->M, in->n_vertices, in->obs_edges);
+  const Layout L = make_layout(D);
+  const BatchView b = points_view(in);
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads)
+  {
+    std::vector<double> ws((size_t)L.total);
+    std::vector<double> lds(4 * NBMAX * NBMAX + 8 + 128);
+    std::vector<int> ilds(2 * NBMAX);
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t p = first; p < first + count; ++p) {
+      HostLane c;
+      c.lds = lds.data();
+      c.ildsp = ilds.data();
+      const ProblemIn pin = problem_view(b, D, p);
+      ObcaSolver<HostLane, 1, MAXE, 1> S(c, D, L, o, pin, ws.data());
+      Result r{};
+      S.run(r);
+      if (out->x)
+        for (int q = 0; q < D.n; ++q) out->x[(size_t)p * D.n + q] = ws[L.x + q];
+      if (out->objective) out->objective[p] = r.objective;
+      if (out->status) out->status[p] = r.status;
+      if (out->iterations) out->iterations[p] = r.iters;
+      if (out->n_factor) out->n_factor[p] = r.n_factor;
+      if (out->nlp_error) out->nlp_error[p] = r.nlp_error;
+      if (out->n_resto) out->n_resto[p] = r.n_resto;
+    }
+  }
+  return 0;
+}
+
 // Reeds-Shepp words for one pose pair on the host (rs_core.h, the same core as htp_rs_all_paths_batch).
 // Used by the workload generator's fish-tail warm starts (synth.py), which run before any GPU call.
 // The reference's rounding (pure-Python reeds_shepp.py): no a*b+c contraction into FMA, as the device build
