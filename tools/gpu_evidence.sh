@@ -60,6 +60,7 @@ for S in "$@"; do
                [ $rc -le 1 ] || exit $rc ;;   # test failures (1) go on; a crash, abort or time limit stops
     pytest:*) files=$(echo "${S#pytest:}" | tr ',' ' ' | sed 's|\([^ ]*\)|tests/\1|g')
               run pytest_sel 900 python -u -m pytest $files -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    e2eC) run e2eC 600 python -u bench.py --e2e --config C --steps 3 --warmup 1 ;;
     ychain) run ychain 600 python -u bench.py --e2e --planner ypark_hastar --steps 3 --warmup 1 ;;
     benchC) run benchC 600 python -u bench.py --config C --steps 6 --no-cpu-baseline ;;
     benchE) run benchE 900 python -u bench.py --config E --steps 1 --warmup 0 --no-cpu-baseline ;;
