@@ -60,6 +60,8 @@ for S in "$@"; do
                [ $rc -le 1 ] || exit $rc ;;   # test failures (1) go on; a crash, abort or time limit stops
     pytest:*) files=$(echo "${S#pytest:}" | tr ',' ' ' | sed 's|\([^ ]*\)|tests/\1|g')
               run pytest_sel 900 python -u -m pytest $files -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    benchAB) run benchA 200 python -u bench.py --config A --steps 2 --no-cpu-baseline
+             run benchB 200 python -u bench.py --config B --steps 6 --no-cpu-baseline ;;
     e2eC) run e2eC 600 python -u bench.py --e2e --config C --steps 3 --warmup 1 ;;
     ychain) run ychain 600 python -u bench.py --e2e --planner ypark_hastar --steps 3 --warmup 1 ;;
     benchC) run benchC 600 python -u bench.py --config C --steps 6 --no-cpu-baseline ;;
