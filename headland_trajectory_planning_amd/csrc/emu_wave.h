@@ -5,8 +5,8 @@
 //   mfma16 ............. v_mfma_f64_16x16x4f64 on the lanes' operands, D = C + A B as a fused multiply-add chain
 //                        over k = 0..3 (the model tests/test_gpu_mfma_model.py pins on the hardware).
 // Built with clang (-ffp-contract=on, FMA enabled) like the device translation unit, so every a * b + c of the
-// source is fused or not fused alike on both; the solver's libm is the correctly rounded htp_libm.h on both
-// (obca_core.h HTP_SOLVER_CRLIBM).  The device solve is then reproduced on the host bit for bit
+// source is fused or not fused alike on both; the solver's libm is the deterministic one on both
+// (obca_core.h HTP_SOLVER_DETLIBM: htp_fastm.h's explicit-FMA sin / cos / tan / log, htp_libm.h's pow).  The device solve is then reproduced on the host bit for bit
 // (tests/test_gpu_emulation.py) -- the witness that a device / oracle divergence is summation order, not a bug.
 // Never part of the product.
 #pragma once

@@ -28,6 +28,7 @@
 #pragma once
 #include <cmath>
 #include "htp_libm.h"
+#include "htp_fastm.h"
 #include <cstdint>
 #ifdef HTP_HA_DEBUG
 #include <cstdio>
@@ -143,9 +144,25 @@ struct Footprint {
   const double* body;  // [nb][2] car-frame vertices (LDS on the device)
   int nb, blk0, blk1, field, lane0, lane1;
 
+  // Exact shortcut of the separating-axis test: a blocker whose bounding box is apart from the body's by more
+  // than SAT_EPS (metres) in x or y is disjoint from it by at least that much, and for the convex rectangles and
+  // quads the planners lower (tree rows, obstacle squares) some edge normal separates them by a comparable
+  // amount, far above rounding -- the full test returns false for it too.
+  static constexpr double SAT_EPS = 1e-6;
   HTP_HD bool sat_hit(const double* bx, const double* by, int p) const {
     const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
     const double* V = g.vert + 2 * o;
+    {
+      double ax0 = bx[0], ax1 = bx[0], ay0 = by[0], ay1 = by[0];
+      for (int j = 1; j < nb; ++j) {
+        ax0 = fmin(ax0, bx[j]); ax1 = fmax(ax1, bx[j]); ay0 = fmin(ay0, by[j]); ay1 = fmax(ay1, by[j]);
+      }
+      double qx0 = V[0], qx1 = V[0], qy0 = V[1], qy1 = V[1];
+      for (int j = 1; j < m; ++j) {
+        qx0 = fmin(qx0, V[2 * j]); qx1 = fmax(qx1, V[2 * j]); qy0 = fmin(qy0, V[2 * j + 1]); qy1 = fmax(qy1, V[2 * j + 1]);
+      }
+      if (qx0 > ax1 + SAT_EPS || ax0 > qx1 + SAT_EPS || qy0 > ay1 + SAT_EPS || ay0 > qy1 + SAT_EPS) return false;
+    }
     for (int k = 0; k < nb; ++k) {  // body edges
       const int k1 = (k + 1) == nb ? 0 : k + 1;
       const double ex = bx[k1] - bx[k], ey = by[k1] - by[k];
@@ -215,8 +232,37 @@ struct Footprint {
     return true;
   }
 
+  // Exact shortcut of in_lanes: the body lies inside ONE lane polygon (convex, CCW) with every corner at least
+  // LANE_EPS (distance, metres) inside every edge line of it.  For such a polygon and each body edge A -> B the
+  // clip of in_lanes computes c0 = cross(A) > 0 with the same expression, and c1 = cross(B) - cross(A) to within
+  // a few ulp of |e| |B - A|, far below the margin: every t = -c0 / c1 is < 0 (c1 > 0) or > 1 (c1 < 0), so the
+  // interval stays [0, 1] and the sweep reaches 1 -- in_lanes returns true with the same doubles.  Poses that
+  // straddle two lane polygons, or come within LANE_EPS of an edge, take the full test.
+  static constexpr double LANE_EPS = 1e-9;
+  mutable int lane_hint = 0;   // the lane polygon that held the last body (any holding polygon gives the result)
+  HTP_HD bool in_one_lane(const double* bx, const double* by) const {
+    const int nl = lane1 - lane0;
+    for (int r = 0; r < nl; ++r) {
+      int p = lane0 + lane_hint + r;
+      if (p >= lane1) p -= nl;
+      const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
+      const double* V = g.vert + 2 * o;
+      bool in = true;
+      for (int i = 0; i < m && in; ++i) {
+        const int j = (i + 1) == m ? 0 : i + 1;
+        const double vx = V[2 * i], vy = V[2 * i + 1];
+        const double ex = V[2 * j] - vx, ey = V[2 * j + 1] - vy;
+        const double tol = LANE_EPS * (fabs(ex) + fabs(ey));
+        for (int k = 0; k < nb && in; ++k) in = ex * (by[k] - vy) - ey * (bx[k] - vx) > tol;
+      }
+      if (in) { lane_hint = p - lane0; return true; }
+    }
+    return false;
+  }
+
   // every body edge covered by the union of the lane polygons (CCW, convex)
   HTP_HD bool in_lanes(const double* bx, const double* by) const {
+    if (in_one_lane(bx, by)) return true;
     const int j0 = lane0, j1 = lane1;
     for (int k = 0; k < nb; ++k) {
       const int k1 = (k + 1) == nb ? 0 : k + 1;
@@ -258,8 +304,13 @@ struct Footprint {
     return true;
   }
 
+  // The footprint's rotation takes htp_fastm.h's sincos (explicit FMA, <= 2 ulp, the same doubles on the device
+  // and the host build), not the double-double libm: only a collision boolean depends on it, and a last-bit
+  // difference flips one only for a body within ~1e-15 m of a boundary (the oracle's numpy cos / sin are not
+  // correctly rounded either).  Trajectory samples and grid indices keep htp_libm.h.
   HTP_HD bool pose_hits(double x, double y, double yaw) const {
-    const double cs = hm::cos(yaw), sn = hm::sin(yaw);
+    double sn, cs;
+    fm::sincos(yaw, sn, cs);
     double bx[MAXB], by[MAXB];
     for (int k = 0; k < nb; ++k) {
       const double vx = body[2 * k], vy = body[2 * k + 1];
@@ -574,8 +625,8 @@ struct Search {
         int dir;
         if (si < 0) { lx = 0.0; ly = 0.0; lyaw = 0.0; }
         else {
-          rs::interp(sh.pd[j], p.typ[si], maxc, sh.org[3 * si], sh.org[3 * si + 1], sh.org[3 * si + 2], lx, ly, lyaw,
-                     cs, dir);
+          rs::interp<true>(sh.pd[j], p.typ[si], maxc, sh.org[3 * si], sh.org[3 * si + 1], sh.org[3 * si + 2], lx, ly,
+                           lyaw, cs, dir);
           if (p.typ[si] == rs::SEG_S) lyaw = sh.org[3 * si + 2];
         }
         const double gx = cq * lx + sq * ly + sx;

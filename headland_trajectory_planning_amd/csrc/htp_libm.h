@@ -1,4 +1,4 @@
-// Correctly rounded libm for the planner cores (sin, cos, tan, atan, atan2, asin, acos, hypot, pow), one
+// Deterministic double-double libm for the planner cores (sin, cos, tan, atan, atan2, asin, acos, hypot, pow), one
 // __host__ __device__ source for the gfx950 kernels and every host build of the same cores.
 //
 // Why: integer outputs of the reference's planners hang on the last bit of a transcendental.  A spline piece
@@ -8,13 +8,16 @@
 // ~0.1 % of sin/cos/atan/atan2/asin/acos/pow arguments; numpy's AVX-512 arctan2/hypot/tan differ from
 // glibc on 7.8 % / 0.6 % / 0.5 %: tools/libm_check.py, profiles/r04_libm_check.json).  Evaluating every
 // function in double-double (error < 2^-100 relative before the final rounding) and rounding once gives the
-// correctly rounded result on both sides of the boundary, so the device and the host builds produce the same
-// doubles by construction.  Arithmetic: explicit fma only (exact on both sides), no contraction.
+// same double on both sides of the boundary (the same operations in the same order), so the device and the
+// host builds produce the same doubles by construction.  There is no Ziv rounding test with a higher-precision
+// fallback: an argument whose exact result lies within 2^-100 of a rounding boundary can still round the wrong
+// way -- identically on both sides.  On 10^7 random arguments per function no misrounding was found
+// (tools/libm_check.py), so "correctly rounded" below means "in every case tested", not a proof.  Arithmetic: explicit fma only (exact on both sides), no contraction.
 //
 // HTP_LIBM_PLATFORM (host builds only): forward to the platform libm instead -- the build that reproduces the
 // reference's own doubles where they were produced by CPython's math module (golden-vector tests).
 //
-// Domain: correctly rounded for finite arguments with |x| < 2^30 (sin, cos, tan) and normal results; C99
+// Domain: double-double accurate for finite arguments with |x| < 2^30 (sin, cos, tan) and normal results; C99
 // special values (zeros, infinities, NaN) follow glibc.  Constants: tools/gen_libm_consts.py (mpmath).
 #pragma once
 #include <cmath>

@@ -23,6 +23,12 @@ namespace {
 
 constexpr int LDS_D = LDS_WAVE_DOUBLES;  // scratch + filter + Riccati stage ring / pivoted blocks (obca_core.h)
 
+// HTP_ONLY44 (experiment variants, tools/build_variants.py): instantiate only the config A-E solver
+// obca_solve_kernel<4, 4, 0> -- one instantiation compiles in a quarter of the time
+#ifndef HTP_ONLY44
+#define HTP_ONLY44 0
+#endif
+
 #ifndef HTP_WAVES_PER_EU
 #define HTP_WAVES_PER_EU 1
 #endif
@@ -297,7 +303,12 @@ int launch_solve(htp_ctx* ctx, const htp_obca_batch* in, const htp_obca_result* 
   Layout L = make_layout(D);
   const bool u44 = uniform44(D);
   const unsigned pad = lds_pad_bytes();
+#if HTP_ONLY44
+  if (!u44) return fail(ctx, "[OBCA] experiment build (HTP_ONLY44): 4-edge polytopes only");
+  const int cap = resident_waves_t<4, 4>(ctx, pad);
+#else
   const int cap = u44 ? resident_waves_t<4, 4>(ctx, pad) : resident_waves_t<MAXE, MAXE>(ctx, pad);
+#endif
   if (cap < 0) return -1;
   if (waves <= 0 || waves > cap) waves = cap;
   if (src.q == nullptr && waves > src.n_static) waves = src.n_static;
@@ -320,10 +331,12 @@ int launch_solve(htp_ctx* ctx, const htp_obca_batch* in, const htp_obca_result* 
     hipLaunchKernelGGL((obca_solve_kernel<4, 4, 0>), dim3((unsigned)waves), dim3(64), pad, s, (const Shape*)ctx->shape, b,
                        (double*)ctx->ws, (int64_t)L.total, res, out->x, src, ov);
   } else {
+#if !HTP_ONLY44
     if (pad) HIPCHK(hipFuncSetAttribute((const void*)obca_solve_kernel<MAXE, MAXE, 0>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad));
     hipLaunchKernelGGL((obca_solve_kernel<MAXE, MAXE, 0>), dim3((unsigned)waves), dim3(64), pad, s,
                        (const Shape*)ctx->shape, b, (double*)ctx->ws, (int64_t)L.total, res, out->x, src, ov);
+#endif
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1, s));
@@ -342,7 +355,11 @@ int32_t htp_obca_resident_waves(htp_ctx* ctx, const htp_obca_batch* in) {
   Dims D;
   make_dims(D, in->N, in->M, in->K, in->time_opt, in->obs_edges, in->body_edges);
   HIPCHK(hipSetDevice(ctx->device));
+#if HTP_ONLY44
+  return resident_waves_t<4, 4>(ctx, lds_pad_bytes());
+#else
   return uniform44(D) ? resident_waves_t<4, 4>(ctx, lds_pad_bytes()) : resident_waves_t<MAXE, MAXE>(ctx, lds_pad_bytes());
+#endif
 }
 
 int htp_obca_solve_batch_device(htp_ctx* ctx, const htp_obca_batch* in, htp_obca_result* out, void* stream) {
@@ -505,6 +522,9 @@ int htp_obca_points_solve_batch_device(htp_ctx* ctx, const htp_obca_points_batch
   if (in->batch == 0) return 0;
   if (!out->x) return fail(ctx, "[OBCA] out->x is required");
   HIPCHK(hipSetDevice(ctx->device));
+#if HTP_ONLY44
+  return fail(ctx, "[OBCA] experiment build (HTP_ONLY44): no point formulation");
+#else
   if (check_idle(ctx, (hipStream_t)stream)) return -1;
   Dims D;
   make_dims_points(D, in->N, in->M, in->n_vertices, in->obs_edges);
@@ -540,6 +560,7 @@ int htp_obca_points_solve_batch_device(htp_ctx* ctx, const htp_obca_points_batch
   HIPCHK(hipEventRecord(ctx->ev1, s));
   ctx->last_queue = nullptr;
   return 0;
+#endif
 }
 
 int htp_obca_points_solve_batch(htp_ctx* ctx, const htp_obca_points_batch* in, htp_obca_result* out) {

@@ -146,6 +146,16 @@ int htp_ypark_hastar_chain_device(htp_ctx* ctx, const htp_ychain_batch* in, void
       !in->status || !in->ypark_out.status || !in->ypark_out.n_path || !in->ypark_out.path || !in->hastar_out.x ||
       !in->hastar_out.y || !in->hastar_out.dir || !in->hastar_out.status || !in->hastar_out.n_path)
     return fail(ctx, "ychain: array missing");
+  // the hybrid A* entry's own host checks, done here before anything is enqueued: k_lower writes into these
+  // pools, and a rejected search must not leave the Y-park search and the lowering already queued
+  const htp_hastar_batch& ha = in->hastar;
+  if (!ha.params || !ha.desc || !ha.poly_off || !ha.vertices || !ha.lane_len || !ha.guide || !ha.motions)
+    return fail(ctx, "ychain: hybrid A* pool missing");
+  if (ha.npoly < 1 || ha.nvert < 1 || ha.nguide < 1 || ha.nmotion < 1 || ha.max_nodes_cap < 0 ||
+      ha.max_nodes_cap > 1000000 || ha.cap_log < 0)
+    return fail(ctx, "ychain: hybrid A* pool sizes");
+  if (!in->hastar_out.counter || !in->hastar_out.yaw || !in->hastar_out.k)
+    return fail(ctx, "ychain: hybrid A* output array missing");
   if (B == 0) return 0;
   HIPCHK(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;

@@ -77,6 +77,11 @@ HTP_HD inline void sincos(double x, double& s, double& c) {
 // 16 is slower again (profiles/r03t_ab_sweep_unroll.txt, r03u_ab_sweep_unroll.txt; results bit-identical)
 // Riccati factor: stop at the first non-positive-definite pivot (the inertia is then decided; 1) or run every stage
 // (0, the round-3 kernel) -- bit-identical results, fewer cycles in inertia-correction trials
+// Riccati factor: stage records staged through LDS HTP_FAC_SB stages at a time (0: one stage of register prefetch,
+// the round-4 kernel; bit-identical either way)
+#ifndef HTP_FAC_SB
+#define HTP_FAC_SB 4
+#endif
 #ifndef HTP_RIC_EARLY_EXIT
 #define HTP_RIC_EARLY_EXIT 1
 #endif
@@ -407,6 +412,7 @@ constexpr int RING_DOUBLES = (RING_SB + 1) * RS_L;
 #endif
 constexpr int PIV_LDS_PER_LANE = HTP_PIV_LDS ? 55 : 0;
 constexpr int LDS_WAVE_DOUBLES = RING_OFF + (RING_DOUBLES > 64 * PIV_LDS_PER_LANE ? RING_DOUBLES : 64 * PIV_LDS_PER_LANE);
+static_assert(HTP_FAC_SB >= 0 && RING_OFF + HTP_FAC_SB * 6 * 64 <= LDS_WAVE_DOUBLES, "factor staging exceeds the ring");
 
 // ---------------------------------------------------------------------------
 template <class Ctx, int EN_ = 4, int EM_ = 4, int FORM_ = 0>
@@ -445,7 +451,9 @@ struct ObcaSolver {
   HTP_HD HTP_FI double hsf() const { return rs ? 0.0 : sf; }
   long long cyc[8];
 #ifdef HTP_KKT_PROF  // experiments: KKT-solve sub-phases (local rhs sweep, stage Riccati solve, local back sweep)
-  long long kprof[3] = {0, 0, 0};
+  // HTP_KKT_PROF=2: finer -- rhs sweep, stage rhs assembly, Riccati backward pass, forward pass, scatter, back
+  // sweep, and the number of KKT solves (reported in Result::cyc 0-3, 5-7)
+  long long kprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define HTP_KPROF(k, t) do { const long long t_ = c.clock(); kprof[k] += t_ - (t); (t) = t_; } while (0)
 #else
 #define HTP_KPROF(k, t) do { } while (0)
@@ -2715,11 +2723,40 @@ struct ObcaSolver {
       c.sync();
     };
     if (ric_relax) relax_regs(N - 1);
-    double hcur[4], fcur[2], hnxt[4], fnxt[2];
+    double hcur[4], fcur[2];
+#if HTP_FAC_SB > 0
+    // Stage records through this lane's slice of the LDS ring (free during the factor): every HTP_FAC_SB stages
+    // one batch of 6 HTP_FAC_SB loads per lane, so the chain waits for memory once per batch instead of once per
+    // stage (a stage's work is shorter than a load's latency under load, and every load also waits for the
+    // previous stages' P / K / chol stores, which the in-order vmcnt counter places before it).  Same values.
+    ld* fring = c.lds + RING_OFF;
+    auto fac_fill = [&](int hi) {   // stages hi, hi - 1, ..., hi - HTP_FAC_SB + 1 (those >= 0)
+      double v[HTP_FAC_SB][6];
+#pragma unroll
+      for (int sb = 0; sb < HTP_FAC_SB; ++sb) {
+        const int st = hi - sb >= 0 ? hi - sb : 0;
+        ld_h(st, v[sb]);
+        ld_f(st, v[sb] + 4);
+      }
+#pragma unroll
+      for (int sb = 0; sb < HTP_FAC_SB; ++sb)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) fring[(sb * 6 + k) * 64 + c.lane] = v[sb][k];
+    };
+    for (int i = N - 2; i >= 0; --i) {
+      HTP_PROF0();
+      const int sb = (N - 2 - i) % HTP_FAC_SB;
+      if (sb == 0) fac_fill(i);
+      for (int r = 0; r < 4; ++r) hcur[r] = fring[(sb * 6 + r) * 64 + c.lane];
+      fcur[0] = fring[(sb * 6 + 4) * 64 + c.lane];
+      fcur[1] = fring[(sb * 6 + 5) * 64 + c.lane];
+#else
+    double hnxt[4], fnxt[2];
     if (N >= 2) { ld_h(N - 2, hcur); ld_f(N - 2, fcur); }
     for (int i = N - 2; i >= 0; --i) {
       HTP_PROF0();
       if (i > 0) { ld_h(i - 1, hnxt); ld_f(i - 1, fnxt); }  // next stage's record, in flight during this one
+#endif
       dbl4 Y = {0.0, 0.0, 0.0, 0.0};
       Y = Ctx::mfma16(Pc[0], fcur[0], Y);
       Y = Ctx::mfma16(Pc[1], fcur[1], Y);
@@ -2756,9 +2793,11 @@ struct ObcaSolver {
       }
       c.sync();
       if (ric_relax) relax_regs(i);
+#if HTP_FAC_SB == 0
       for (int r = 0; r < 4; ++r) hcur[r] = hnxt[r];
       fcur[0] = fnxt[0];
       fcur[1] = fnxt[1];
+#endif
       HTP_PROF(5);
       // A non-positive-definite pivot decides the inertia (wrong: factor_ic perturbs and re-factors; the point
       // formulation's block LDL^T re-derives it from the assembled blocks): the remaining stages are not needed.
@@ -2934,6 +2973,9 @@ struct ObcaSolver {
   }
 
   HTP_HD HTP_FI void riccati_solve_mfma(const gd* V, gd* X) {
+#if defined(HTP_KKT_PROF) && HTP_KKT_PROF == 2
+    long long kt_ric = c.clock();
+#endif
     const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
     const int col = c.lane & 15, rg = c.lane >> 4;
     const bool c0 = col == 0;
@@ -3031,6 +3073,9 @@ struct ObcaSolver {
     }
     c.sync();
     HTP_PROF(6);
+#if defined(HTP_KKT_PROF) && HTP_KKT_PROF == 2
+    { const long long t_ = c.clock(); kprof[2] += t_ - kt_ric; kt_ric = t_; }
+#endif
     // ---------------- forward: z_0 = [V_0[0:5] / sc; 0]
     const gd* scE = A(L.scE);
     dbl4 zu = {0.0, 0.0, 0.0, 0.0};  // [z_i; v_i] in column 0
@@ -3109,6 +3154,9 @@ struct ObcaSolver {
     }
     c.sync();
     HTP_PROF(7);
+#if defined(HTP_KKT_PROF) && HTP_KKT_PROF == 2
+    kprof[3] += c.clock() - kt_ric;
+#endif
   }
 #endif
 
@@ -3614,6 +3662,9 @@ struct ObcaSolver {
     local_rhs_sweep<EN_, EM_>(ls, dw, dc, bx, bs, bc, bd);
     c.sync();
     HTP_KPROF(0, tk);
+#if defined(HTP_KKT_PROF) && HTP_KKT_PROF == 2
+    kprof[6] += 1;
+#endif
     const gd* PR = A(L.pairR);
     const gd* scE = A(L.scE);
     gd* V = A(L.V);
@@ -3650,6 +3701,9 @@ struct ObcaSolver {
     if constexpr (PT)
       for (int e = c.lane; e < nb; e += c.width) V[(int64_t)N * nb + e] = (e < NS) ? bc[D.eTerm + e] : 0.0;
     c.sync();
+#if defined(HTP_KKT_PROF) && HTP_KKT_PROF == 2
+    HTP_KPROF(1, tk);
+#endif
     gd* X = A(L.X);
     if (use_ric) {
       if constexpr (PT) ric_solve_terminal(V, X);
@@ -3714,10 +3768,18 @@ struct ObcaSolver {
       }
     }
     c.sync();
+#if defined(HTP_KKT_PROF) && HTP_KKT_PROF == 2
+    HTP_KPROF(4, tk);
+#else
     HTP_KPROF(1, tk);
+#endif
     local_back_sweep<EN_, EM_>(ls, dw, dc, bx, bs, bc, bd, ox, os, oc, od);
     c.sync();
+#if defined(HTP_KKT_PROF) && HTP_KKT_PROF == 2
+    HTP_KPROF(5, tk);
+#else
     HTP_KPROF(2, tk);
+#endif
     if (rs) {  // dn = (b_n - dy) / (S_n + dw), dp = (b_p + dy) / (S_p + dw)
       double sn_[SW_U], sp_[SW_U], dy_[SW_U], bn_[SW_U], bp_[SW_U];
       sweep(D.mc + D.md, [&](int r, int k) {
@@ -4369,7 +4431,12 @@ struct ObcaSolver {
         if (k != 4) res.cyc[k] = pcyc[k];
 #endif
 #ifdef HTP_KKT_PROF
+#if HTP_KKT_PROF == 2
+      const int slot[7] = {0, 1, 2, 3, 5, 6, 7};
+      for (int k = 0; k < 7; ++k) res.cyc[slot[k]] = kprof[k];
+#else
       for (int k = 0; k < 3; ++k) res.cyc[5 + k] = kprof[k];
+#endif
 #endif
       res.cyc[4] = c.clock() - t0;
     }

@@ -25,6 +25,7 @@
 #endif
 
 #include "htp_libm.h"
+#include "htp_fastm.h"
 
 namespace htp {
 namespace rs {
@@ -385,20 +386,30 @@ HTP_HD inline void generate_paths(double sx, double sy, double syaw, double gx, 
 }
 
 // interpolate (:533-562) for one point
+// FAST: the sin / cos of htp_fastm.h (explicit FMA, <= 2 ulp, the same doubles on the device and every host build)
+// for callers whose samples only feed a collision boolean (the hybrid A* goal shot's per-sample footprint test,
+// hastar_core.h rs_path_hits); every sample the library returns is produced with FAST = false.
+template <bool FAST = false>
 HTP_HD inline void interp(double l, int m, double maxc, double ox, double oy, double oyaw, double& px, double& py,
                           double& pyaw, double& cs, int& dir) {
   if (m == SEG_S) {
-    px = ox + l / maxc * hm::cos(oyaw);
-    py = oy + l / maxc * hm::sin(oyaw);
+    double so, co;
+    if constexpr (FAST) fm::sincos(oyaw, so, co);
+    else { co = hm::cos(oyaw); so = hm::sin(oyaw); }
+    px = ox + l / maxc * co;
+    py = oy + l / maxc * so;
     pyaw = oyaw;
     cs = 0.0;
   } else {
-    const double ldx = hm::sin(l) / maxc;
+    double sl, cl, sm, cm;   // sin / cos of l and of -oyaw
+    if constexpr (FAST) { fm::sincos(l, sl, cl); fm::sincos(-oyaw, sm, cm); }
+    else { sl = hm::sin(l); cl = hm::cos(l); sm = hm::sin(-oyaw); cm = hm::cos(-oyaw); }
+    const double ldx = sl / maxc;
     double ldy;
-    if (m == SEG_L) { ldy = (1.0 - hm::cos(l)) / maxc; cs = maxc; }
-    else { ldy = (1.0 - hm::cos(l)) / (-maxc); cs = -maxc; }
-    const double gdx = hm::cos(-oyaw) * ldx + hm::sin(-oyaw) * ldy;
-    const double gdy = -hm::sin(-oyaw) * ldx + hm::cos(-oyaw) * ldy;
+    if (m == SEG_L) { ldy = (1.0 - cl) / maxc; cs = maxc; }
+    else { ldy = (1.0 - cl) / (-maxc); cs = -maxc; }
+    const double gdx = cm * ldx + sm * ldy;
+    const double gdy = -sm * ldx + cm * ldy;
     px = ox + gdx;
     py = oy + gdy;
   }

@@ -507,11 +507,12 @@ int htp_ypark_hastar_chain_device(htp_ctx* ctx, const htp_ychain_batch* in, void
 /* Per-stage kernel times (ms) of the last chain: Y-park, lowering, hybrid A*, init guess + resample. */
 int htp_ychain_last_ms(htp_ctx* ctx, double* ms4);
 
-/* ---- correctly rounded libm of the planner cores (csrc/htp_libm.h) ----------------------------------------
+/* ---- deterministic double-double libm of the planner cores (csrc/htp_libm.h) ----------------------------------------
  * Replaces nothing in the reference: the reference's planners call CPython's math module / numpy (glibc, or
  * numpy's SIMD kernels), whose last bits differ between platforms.  Every device planner kernel and every host
  * build of the same cores evaluates sin, cos, tan, atan, atan2, asin, acos, hypot and pow with this one
- * correctly rounded implementation, so integer outputs that hang on the last bit (a spline piece's sample
+ * double-double implementation (< 2^-100 relative before one final rounding, no Ziv fallback; the same
+ * operations on both sides, so the same doubles), so integer outputs that hang on the last bit (a spline piece's sample
  * count, R/path_planner/utils/cubic_spline.py:102) are identical on the GPU and on the host.
  * fn: 0 sin, 1 cos, 2 tan, 3 atan, 4 atan2(x[i], y[i]), 5 asin, 6 acos, 7 hypot(x[i], y[i]), 8 pow(x[i], y[i]), 9 log; the solver's
  * fast deterministic functions (htp_fastm.h, <= 2 ulp): 10 log, 11 sin, 12 cos, 13 tan.

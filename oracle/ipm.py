@@ -65,6 +65,8 @@ import numpy as np
 import scipy.linalg as sla
 import scipy.sparse as sp
 
+from oracle import libm
+
 EPS = np.finfo(float).eps
 
 OPTS = dict(
@@ -434,7 +436,7 @@ class _Ipm:
                 return np.inf
         val = p.f(x, mu)
         for v, m in zip(sl, masks):
-            val -= mu * np.sum(np.log(v[m]))
+            val -= mu * np.sum(libm.log(v[m]))
         kd = o["kappa_d"] * mu
         val += kd * np.sum(sl[0][p.hxL & ~p.hxU]) + kd * np.sum(sl[1][p.hxU & ~p.hxL])
         val += kd * np.sum(sl[2][p.hdL & ~p.hdU]) + kd * np.sum(sl[3][p.hdU & ~p.hdL])

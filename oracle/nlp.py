@@ -28,6 +28,8 @@ import numpy as np
 import scipy.sparse as sp
 import sympy
 
+from oracle import libm
+
 NS, NC = 5, 2
 SLACK_WEIGHT = 5000.0  # optimizer.py:472
 
@@ -57,9 +59,10 @@ def _dyn_funcs(topt):
     phi = sum(ys[k] * F[k] for k in range(5))
     H = sympy.hessian(phi, w)
     args = w + [dT, L] + list(ys)
-    fF = sympy.lambdify(args, list(F), "numpy")
-    fJ = sympy.lambdify(args, [J[i, j] for i in range(5) for j in range(len(w))], "numpy")
-    fH = sympy.lambdify(args, [H[i, j] for i in range(len(w)) for j in range(len(w))], "numpy")
+    mods = [{"sin": libm.sin, "cos": libm.cos, "tan": libm.tan}, "numpy"]   # oracle/libm.py: numpy or glibc
+    fF = sympy.lambdify(args, list(F), mods)
+    fJ = sympy.lambdify(args, [J[i, j] for i in range(5) for j in range(len(w))], mods)
+    fH = sympy.lambdify(args, [H[i, j] for i in range(len(w)) for j in range(len(w))], mods)
     return fF, fJ, fH, len(w)
 
 
@@ -306,7 +309,7 @@ class ObcaNLP:
             mu = x[mu0[:, None] + np.arange(len(g))]
             st = X[i]
             w = la @ A
-            c, sn = np.cos(st[:, 3]), np.sin(st[:, 3])
+            c, sn = libm.cos(st[:, 3]), libm.sin(st[:, 3])
             r = self.gCol + 4 * sel
             out[r] = w[:, 0] * w[:, 0] + w[:, 1] * w[:, 1]
             out[r + 1] = mu @ G[:, 0] + (c * w[:, 0] + sn * w[:, 1])
@@ -347,7 +350,7 @@ class ObcaNLP:
             la = x[la0[:, None] + np.arange(em)]
             st = X[i]
             w = la @ A
-            c, sn = np.cos(st[:, 3]), np.sin(st[:, 3])
+            c, sn = libm.cos(st[:, 3]), libm.sin(st[:, 3])
             r = (self.gCol + 4 * sel)[:, None]
             lai = la0[:, None] + np.arange(em)
             mui = mu0[:, None] + np.arange(en)
@@ -434,7 +437,7 @@ class ObcaNLP:
             y1, y2a, y2b, y3 = y[r], y[r + 1], y[r + 2], y[r + 3]
             la = x[la0[:, None] + np.arange(em)]
             w = la @ A
-            c, sn = np.cos(X[i, 3]), np.sin(X[i, 3])
+            c, sn = libm.cos(X[i, 3]), libm.sin(X[i, 3])
             lai = la0[:, None] + np.arange(em)
             th = NS * i + 3
             AA = 2.0 * A @ A.T

@@ -7,6 +7,12 @@ already end at different statuses or points, the reference algorithm itself does
 rounding level, and the device's different-but-valid ending is the same phenomenon.
 
     python tests/golden/make_witness.py D347 E84 E6 P19     -> tests/golden/witness/<name>.npz
+
+Libm witnesses (oracle/libm.py): the same oracle, the same KKT elimination (StructuredKKT) and the same
+instance, with the transcendental functions taken from glibc (CPython's math module -- the functions CasADi's
+SX VM calls in the reference's own solve) instead of numpy's AVX-512 kernels:
+
+    python tests/golden/make_witness.py E12:glibc E54:glibc  -> tests/golden/witness/<name>_libm.npz
 """
 import os
 import sys
@@ -23,6 +29,8 @@ OUT = os.path.join(ROOT, "tests", "golden", "witness")
 def run(name):
     from oracle.ipm import IpoptRestatement
     t = time.time()
+    if name.endswith(":glibc"):
+        return run_libm(name.split(":")[0], t)
     if name.startswith("P"):   # point formulation, tests/test_gpu_points.py small instances (N=12, M=2)
         from headland_trajectory_planning_amd import synth
         from oracle.nlp_points import PointNLP
@@ -52,6 +60,30 @@ def run(name):
              seconds=time.time() - t)
     d = float(np.max(np.abs(a["x"][:5 * N] - b["x"][:5 * N])))
     return (f"{name}: {orders[0]} status {a['status']} it {a['iters']} resto {a['n_resto']} | {orders[1]} status "
+            f"{b['status']} it {b['iters']} resto {b['n_resto']} | max state diff {d:.3g} ({time.time() - t:.0f} s)")
+
+
+def run_libm(name, t):
+    from _fixture_io import load_instance
+    from oracle import libm
+    from oracle.ipm import IpoptRestatement
+    from oracle.nlp import ObcaNLP
+    from oracle.structured import StructuredKKT
+    g = np.load(os.path.join(ROOT, "tests", "golden", "obca_full", f"{name}.npz"))
+    nlp = ObcaNLP(load_instance(g))
+    N = int(g["N"])
+    a = {"x": g["states"], "status": int(g["status"]), "iters": int(g["iters"]), "n_resto": int(g["n_resto"])}
+    libm.set_mode("glibc")
+    b = IpoptRestatement(nlp, kkt=StructuredKKT(nlp)).solve()
+    libm.set_mode("numpy")
+    orders = ("StructuredKKT/numpy-libm", "StructuredKKT/glibc-libm")
+    os.makedirs(OUT, exist_ok=True)
+    np.savez(os.path.join(OUT, f"{name}_libm.npz"), orders=np.array(orders),
+             states_a=a["x"][:5 * N], status_a=a["status"], iters_a=a["iters"], n_resto_a=a["n_resto"],
+             states_b=b["x"][:5 * N], status_b=b["status"], iters_b=b["iters"], n_resto_b=b["n_resto"],
+             seconds=time.time() - t)
+    d = float(np.max(np.abs(a["x"][:5 * N] - b["x"][:5 * N])))
+    return (f"{name} libm: numpy status {a['status']} it {a['iters']} resto {a['n_resto']} | glibc status "
             f"{b['status']} it {b['iters']} resto {b['n_resto']} | max state diff {d:.3g} ({time.time() - t:.0f} s)")
 
 

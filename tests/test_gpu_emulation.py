@@ -1,7 +1,7 @@
 """The device solver reproduced on the host bit for bit.  csrc/htp_emusim.cpp runs the kernel's ObcaSolver
 instantiation on 64 lane threads (csrc/emu_wave.h) with the device's wave-reduction order, the matrix core's
 rounding (tests/test_gpu_mfma_model.py pins the model), the device build's contraction and the shared
-correctly rounded libm; it must return the device's doubles exactly -- solution vector, objective, status,
+deterministic solver libm (obca_core.h HTP_SOLVER_DETLIBM: htp_fastm.h sin / cos / tan / log, htp_libm.h pow); it must return the device's doubles exactly -- solution vector, objective, status,
 iteration and restoration counts:
 
   * live on short solves (configs A, C, D and small restoration cases, both formulations);

@@ -36,6 +36,11 @@ for rnd in range(2):
             tail = ["rhs_sweep", "ric_solve", "back_sweep"] if "kprof" in k else ["errors", "linesearch", "update"]
             head = ["build", "ldlt", "schur"] if "lprof" in k else ["local", "assemble", "chain"]
             nm = head + ["kktsolve", "total"] + tail
+            if "kp2" in k:   # HTP_KKT_PROF=2: rhs sweep, stage rhs, Riccati backward, forward, ric+scatter, back sweep, n_kkt
+                nm = ["rhs_sweep", "stage_rhs", "ric_bwd", "ric_fwd", "total", "ric+scatter", "back_sweep", "n_kkt"]
+                line += " | kkt solves per iteration %.3f" % (cyc[:, 7].sum() / max(1, r.iterations.sum()))
+            if "prof" in k and "kprof" not in k:   # HTP_PROF_ON: stage-chain sub-steps (factor 1/3/5, solve 6/7)
+                nm = ["p0", "fac_mfma", "p2", "fac_chol", "total", "fac_tail", "solve_bwd*", "solve_fwd"]
             line += " | " + " ".join(f"{nm[j]} {cyc[:, j].sum() / tot:.3f}" for j in (0, 1, 2, 3, 5, 6, 7))
             line += " | per-iter cycles %.3g" % (cyc[:, 4] / np.maximum(1, r.iterations)).mean()
         print(line, flush=True)

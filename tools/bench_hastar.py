@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--max-nodes", type=int, default=400)
     ap.add_argument("--cpu-sample", type=int, default=64)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiled runs)")
     args = ap.parse_args()
     import torch
 
@@ -81,9 +82,9 @@ def main():
     npose = int(out["n_pose"].sum().item())
     kms = float(np.mean(ms))
     # CPU baseline: serial host build of the same core on the first problems
-    n = min(args.cpu_sample, B)
+    n = 0 if args.no_cpu else min(args.cpu_sample, B)
     t = time.perf_counter()
-    hres = H.hastar_host(probs[:n])
+    hres = H.hastar_host(probs[:n]) if n else None
     cpu_s = time.perf_counter() - t
     line = {"metric": "hybrid A* headland searches/s (King, res 0.2, max_nodes %d)" % args.max_nodes,
             "value": B / (kms / 1e3), "unit": "searches/s", "batch": B, "kernel_ms": kms, "wall_ms": wall * 1e3,
@@ -93,7 +94,8 @@ def main():
             "workload": f"{len(uniq)} unique collision-free start/goal scenarios (tests/_ha_util.scenario, "
                         f"{skipped} blocked seeds skipped) repeated to {B}",
             "gen_s": gen_s,
-            "cpu_baseline": {"value": n / cpu_s, "unit": "searches/s", "cores": 1, "kind": "port",
+            "cpu_baseline": None if not n else
+                            {"value": n / cpu_s, "unit": "searches/s", "cores": 1, "kind": "port",
                              "sample": f"first {n} searches, serial host build of csrc/hastar_core.h (g++ -O2)",
                              "pose_tests_per_s": float(hres.n_pose.sum()) / cpu_s}}
     print(json.dumps(line))

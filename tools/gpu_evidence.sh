@@ -79,6 +79,13 @@ for S in "$@"; do
     fx:*) IFS=: read -r _ names vars <<< "$S"
           run fx 900 python -u tools/fixture_probe.py $names $vars ;;
     counters) run counters 120 rocprofv3 --list-avail ;;
+    hakt) run hakt 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_hakt -o hakt -- python3 tools/bench_hastar.py --no-cpu
+          run ypkt 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_ypkt -o ypkt -- python3 tools/bench_ypark.py ;;
+    hapmc) for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA" \
+                      "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VALU_TRANS_F64 SQ_WAVES SQ_INSTS_VALU_FMA_F64"; do
+             n=$(echo $grp | cut -c1-12 | tr ' ' '_')
+             run hapmc_$n 180 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${T}_hapmc_$n -o pmc -- python3 tools/bench_hastar.py --no-cpu --steps 1 --warmup 0
+           done ;;
     tail) run tailgen 300 python -u bench.py --gen-only --cache /tmp/htp_instcache
           run tail 600 python -u tools/tail_probe.py D 32768 /tmp/htp_instcache gpurun_out/${T}_tail_D.npz ;;
     *) echo "unknown step $S"; exit 2 ;;
