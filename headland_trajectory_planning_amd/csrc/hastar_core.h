@@ -47,6 +47,10 @@ namespace ha {
 constexpr int MAXB = 8;       // body polygon vertices
 constexpr int MAXMOT = 16;    // motion primitives (King: 14, Pawn: 8)
 constexpr int MAXTRAJ = 64;   // poses per motion primitive (round(L/res) + 1)
+// Poses of one expansion's rollouts held in LDS (every primitive of a search length shares n + 1 poses, stored
+// primitive-major at stride n + 1): nmot (n + 1) <= TRAJCAP.  The reference's settings need 14 x 16 = 224 (King,
+// search length 1.5 m at 0.1 m); 512 keeps a search's LDS at ~21 KB, 7 resident searches per CU instead of 4.
+constexpr int TRAJCAP = 512;
 constexpr int MAXJ = 32;      // lane polygons
 constexpr int MAXCHAIN = 1 << 20;
 constexpr double PI = 3.141592653589793;
@@ -110,7 +114,7 @@ struct Out {
 // Wave-shared scratch (LDS on the device).
 struct Shared {
   double body[MAXB * 2];
-  double traj[MAXMOT * MAXTRAJ * 3];
+  double traj[TRAJCAP * 3];
   int32_t hit[MAXMOT];
   double ccost[MAXMOT];
   double ccurv[MAXMOT];
@@ -498,7 +502,7 @@ struct Search {
     const double delta = stop - init_yaw;
     const double step = delta / div;
     double ax = 0.0, ay = 0.0;
-    double* T = sh.traj + m * MAXTRAJ * 3;
+    double* T = sh.traj + m * (n + 1) * 3;
     for (int i = 0; i <= n; ++i) {  // numpy linspace (step == 0 branch included), angle_wrap, cumsum
       const double yi = (step == 0) ? ((double)i / div) * delta + init_yaw : (double)i * step + init_yaw;
       const double wy = angle_wrap(yi);
@@ -517,7 +521,7 @@ struct Search {
   // simulated_path_cost :306-329 for primitive m (trajectory in sh.traj)
   HTP_HD double motion_cost(int m, int n, const Node& par) const {
     const double steer = g.motion[2 * (dsc[D_MOT0] + m)], dir = g.motion[2 * (dsc[D_MOT0] + m) + 1];
-    const double* T = sh.traj + m * MAXTRAJ * 3;
+    const double* T = sh.traj + m * (n + 1) * 3;
     double cost = par.cost;
     double pl = 0.0;
     for (int i = 0; i < n; ++i) {
@@ -991,7 +995,7 @@ struct Search {
       // expansion: all primitives share the parent's search length
       const double L = search_length(cur.x, cur.y);
       const int n = (int)rint(L / res);
-      if (n < 1 || n + 1 > MAXTRAJ) { status = ST_BAD_INPUT; break; }
+      if (n < 1 || n + 1 > MAXTRAJ || nmot * (n + 1) > TRAJCAP) { status = ST_BAD_INPUT; break; }
       for (int m = c.lane; m < nmot; m += C::width) {
         simulate(m, cur.x, cur.y, cur.yaw, n);
         sh.hit[m] = 0;
@@ -1000,7 +1004,7 @@ struct Search {
       const int tot = nmot * (n + 1);
       for (int q = c.lane; q < tot; q += C::width) {
         const int m = q / (n + 1), i = q - m * (n + 1);
-        const double* T = sh.traj + (m * MAXTRAJ + i) * 3;
+        const double* T = sh.traj + (m * (n + 1) + i) * 3;
         if (pose_hits(T[0], T[1], T[2])) sh.hit[m] = 1;
       }
       o.n_pose += tot;
@@ -1010,7 +1014,7 @@ struct Search {
         sh.ccost[m] = motion_cost(m, n, cur);
         const double steer = g.motion[2 * (dsc[D_MOT0] + m)];
         sh.ccurv[m] = hm::tan(steer) / wb;
-        const double* T = sh.traj + (m * MAXTRAJ + n) * 3;
+        const double* T = sh.traj + (m * (n + 1) + n) * 3;
         index(T[0], T[1], T[2], sh.ckey + 3 * m);
       }
       c.sync();
@@ -1025,7 +1029,7 @@ struct Search {
         if (state == 1 && !(cost < w.node[w.slot[s2].node].cost)) continue;
         const int id = new_node(nn);
         if (id < 0) { cap = true; break; }
-        const double* T = sh.traj + (m * MAXTRAJ + n) * 3;
+        const double* T = sh.traj + (m * (n + 1) + n) * 3;
         Node ch{};
         ch.x = T[0]; ch.y = T[1]; ch.yaw = T[2]; ch.cost = cost; ch.curv = sh.ccurv[m];
         ch.kx = k[0]; ch.ky = k[1]; ch.kt = k[2];
@@ -1095,7 +1099,7 @@ struct Search {
         c.sync();
         const double dir = g.motion[2 * (dsc[D_MOT0] + nd.aux) + 1];
         const double kv = hm::tan(g.motion[2 * (dsc[D_MOT0] + nd.aux)]) / wb;
-        const double* T = sh.traj + nd.aux * MAXTRAJ * 3;
+        const double* T = sh.traj + nd.aux * (n + 1) * 3;
         for (int i = c.lane; i <= n; i += C::width)
           if (off + i < cap_path) {
             px[off + i] = T[3 * i]; py[off + i] = T[3 * i + 1]; pyaw[off + i] = T[3 * i + 2];

@@ -151,3 +151,53 @@ extern "C" int htp_cpu_ychain_lower(const double* rows, int32_t nrows, const dou
   }
   return 0;
 }
+
+// Hybrid A* on the host cores (hastar_core.h, the same core as htp_hastar_search_batch, fp-contract off as the
+// device build): searches [first, first + count) of a batch, one search per OpenMP thread -- the CPU baseline of
+// tools/bench_hastar.py.  Outputs as htp_hastar_result (path arrays may be null: no backtrack).
+#include "hastar_core.h"
+
+extern "C" int htp_cpu_hastar_range(const htp_hastar_batch* in, htp_hastar_result* out, int64_t first, int64_t count,
+                                    int nthreads) {
+  if (!in || !out || first < 0 || count < 0 || first + count > in->batch || in->max_nodes_cap < 0) return -1;
+  using namespace htp::ha;
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+  const int64_t cn = 4 + (int64_t)(in->max_nodes_cap + 1) * MAXMOT + 4;
+  int64_t cs = 1;
+  while (cs < 2 * cn) cs <<= 1;
+  const Geo g{in->poly_off, in->vertices, in->lane_len, in->guide, in->motions};
+#pragma omp parallel num_threads(nthreads)
+  {
+    std::vector<Node> nodes((size_t)cn);
+    std::vector<Slot> slots((size_t)cs);
+    std::vector<double> hval((size_t)cn);
+    std::vector<int32_t> hslot((size_t)cn);
+    std::vector<double> dub((size_t)DUBW * (CAP_DUB + 16));
+    Shared* sh = new Shared();
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t b = first; b < first + count; ++b) {
+      const double* prm = in->params + b * HTP_HA_NPARAM;
+      const int32_t* d = in->desc + b * HTP_HA_NDESC;
+      HostLane c;
+      Work w{nodes.data(), slots.data(), hval.data(), hslot.data(), (int32_t)cn, (int32_t)cs, dub.data(), CAP_DUB};
+      Search<HostLane> S(c, prm, d, g, w, *sh);
+      Out o{};
+      S.run(o, nullptr, 0);
+      int n_path = 0;
+      if (out->x && (o.status == ST_FOUND || o.status == ST_NO_PATH || o.status == ST_MAX_NODES)) {
+        const int64_t off = b * in->cap_path;
+        int st = o.status;
+        n_path = S.backtrack(w.hslot, w.cap_node, out->x + off, out->y + off, out->yaw + off, out->dir + off,
+                             out->k + off, in->cap_path, st);
+        o.status = st;
+      }
+      if (out->status) out->status[b] = o.status;
+      if (out->counter) out->counter[b] = o.counter;
+      if (out->n_path) out->n_path[b] = n_path;
+      if (out->n_expanded) out->n_expanded[b] = o.n_expanded;
+      if (out->n_pose) out->n_pose[b] = o.n_pose;
+    }
+    delete sh;
+  }
+  return 0;
+}

@@ -44,8 +44,22 @@ HTP_HD inline double estrin7(const double* c, double z, double z2, double z4) {
                   std::fma(std::fma(c[3], z, c[2]), z2, std::fma(c[1], z, c[0])));
 }
 
-HTP_HD inline double log(double x) {
-  if (!(x > 0.0) || x == __builtin_huge_val()) return hm::log(x);   // 0, negative, NaN, +inf
+// The rare arguments go to htp_libm.h through out-of-line calls that return by value, so the fast paths below
+// inline into the solver's loops without the double-double code (the compiler would otherwise outline the whole
+// function, and every call site pays the caller-saved register spills of a 512-register kernel).
+#if defined(__GNUC__) || defined(__clang__)
+#define HTP_FM_NOINLINE __attribute__((noinline))
+#define HTP_FM_INLINE __attribute__((always_inline)) inline
+#else
+#define HTP_FM_NOINLINE
+#define HTP_FM_INLINE inline
+#endif
+struct SinCos { double s, c; };
+HTP_HD HTP_FM_NOINLINE double log_slow(double x) { return hm::log(x); }
+HTP_HD HTP_FM_NOINLINE SinCos sincos_slow(double x) { SinCos r; hm::sincos(x, r.s, r.c); return r; }
+
+HTP_HD HTP_FM_INLINE double log(double x) {
+  if (!(x > 0.0) || x == __builtin_huge_val()) return log_slow(x);   // 0, negative, NaN, +inf
   int e;
   double m = std::frexp(x, &e);           // x = m 2^e, m in [0.5, 1) (subnormals included)
   if (m < SQRT1_2) { m *= 2.0; --e; }     // m in [sqrt(1/2), sqrt 2)
@@ -64,8 +78,8 @@ HTP_HD inline double log(double x) {
 constexpr double PIO2_A = 1.57079632673412561417e+00, PIO2_B = 6.07710050630396597660e-11,
                  PIO2_C = 2.02226624879595063154e-21, INV_PIO2 = 6.36619772367581382433e-01;
 
-HTP_HD inline void sincos(double x, double& s, double& c) {
-  if (!(std::fabs(x) < 0x1p20)) { hm::sincos(x, s, c); return; }   // large, inf, NaN
+HTP_HD HTP_FM_INLINE void sincos(double x, double& s, double& c) {
+  if (!(std::fabs(x) < 0x1p20)) { const SinCos r = sincos_slow(x); s = r.s; c = r.c; return; }   // large, inf, NaN
   const double k = rint(x * INV_PIO2);
   const double r = std::fma(-k, PIO2_C, std::fma(-k, PIO2_B, std::fma(-k, PIO2_A, x)));
   const int q = (int)((long long)k & 3);
@@ -76,9 +90,9 @@ HTP_HD inline void sincos(double x, double& s, double& c) {
   if (q & 2) s = -s;
   if (((q + 1) & 2) != 0) c = -c;
 }
-HTP_HD inline double sin(double x) { double s, c; sincos(x, s, c); return s; }
-HTP_HD inline double cos(double x) { double s, c; sincos(x, s, c); return c; }
-HTP_HD inline double tan(double x) { double s, c; sincos(x, s, c); return s / c; }
+HTP_HD HTP_FM_INLINE double sin(double x) { double s, c; sincos(x, s, c); return s; }
+HTP_HD HTP_FM_INLINE double cos(double x) { double s, c; sincos(x, s, c); return c; }
+HTP_HD HTP_FM_INLINE double tan(double x) { double s, c; sincos(x, s, c); return s / c; }
 
 }  // namespace fm
 }  // namespace htp

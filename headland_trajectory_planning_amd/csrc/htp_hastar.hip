@@ -75,8 +75,12 @@ __device__ bool valid(const Pools& P, const double* prm, const int32_t* d, int m
   if (!(res > 0) || !(prm[P_YAWRES] > 0) || !(prm[P_WB] > 0) || !(prm[P_CURV] > 0)) return false;
   const double mn = prm[P_MAXNODES];
   if (!(mn >= 0) || mn > (double)max_nodes_cap) return false;
-  // every search length must give 1 <= round(L/res) and round(L/res)+1 <= MAXTRAJ
-  auto len_ok = [&](double L) { const double n = rint(L / res); return n >= 1 && n + 1 <= MAXTRAJ; };
+  // every search length must give 1 <= round(L/res), round(L/res)+1 <= MAXTRAJ and nmot (round(L/res)+1) <= TRAJCAP
+  const int nmot = d[D_MOT1] - d[D_MOT0];
+  auto len_ok = [&](double L) {
+    const double n = rint(L / res);
+    return n >= 1 && n + 1 <= MAXTRAJ && (double)nmot * (n + 1) <= (double)TRAJCAP;
+  };
   if (!len_ok(prm[P_DEFLEN])) return false;
   for (int p = d[D_LANE0]; p < d[D_LANE1]; ++p)
     if (!len_ok(P.g.lane_len[p])) return false;

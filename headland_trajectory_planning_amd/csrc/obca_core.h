@@ -90,6 +90,9 @@ HTP_HD inline void sincos(double x, double& s, double& c) {
 #ifndef HTP_NAN_GUARD
 #define HTP_NAN_GUARD 1
 #endif
+#ifndef HTP_FUSE_RHS
+#define HTP_FUSE_RHS 1
+#endif
 #ifndef HTP_IC_SCAN
 #define HTP_IC_SCAN 1
 #endif
@@ -398,6 +401,11 @@ HTP_HD inline void bk_solve_packed(T* K, const int* ip, int n, double* v) {
 #ifndef HTP_RING_SB
 #define HTP_RING_SB 8
 #endif
+// ring_fill: lane-major copy with the record sources resolved once per lane (1) or the element-major copy of the
+// round-4 kernel (0); the ring receives the same values
+#ifndef HTP_RING_FILL_LANE
+#define HTP_RING_FILL_LANE 1
+#endif
 constexpr int RING_SB = HTP_RING_SB;             // stages per block
 constexpr int RS_SLOT = 142;                     // LD slot prefix (P | K | chol | J | 1/sc)
 constexpr int RS_V = RS_SLOT, RS_X = RS_SLOT + NBMAX;
@@ -442,6 +450,9 @@ struct ObcaSolver {
   // on that block, with no zero pivot) -- the same delta_w sequence and the same accepted factorization.
   bool ic_scan = false;
   int ic_skip = 0;
+  // HTP_FUSE_RHS: the Newton step's local right-hand-side sweep runs inside the factor sweep (the blocks are
+  // built and factored there already); kkt_solve then skips it.  The same per-block arithmetic: bit-identical.
+  bool fuse_rhs = false;
   // restoration phase (oracle/ipm.py RestoProblem): the iterate is [x, R] with R = [n_c | p_c | n_d | p_d] >= 0,
   // constraints c(x) + n_c - p_c = 0, d(x) + n_d - p_d - s = 0, objective rho sum R + eta/2 |D_R (x - x_R)|^2
   bool rs = false;
@@ -458,14 +469,25 @@ struct ObcaSolver {
 #else
 #define HTP_KPROF(k, t) do { } while (0)
 #endif
+#ifdef HTP_LPROF  // experiments: the local factor sweep -- pass 1 / pass 2 / inertia-scan cycles, trip counts (Result::cyc)
+  long long lprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define HTP_LP(k, v) do { lprof[k] += (v); } while (0)
+#else
+#define HTP_LP(k, v) do { } while (0)
+#endif
 #ifdef HTP_PROF_ON  // experiments: sub-step cycle counters of the stage chain (tools/build_variants.py)
   long long pcyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  long long tprof = 0;
+  long long spcyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // solve passes: ring fills / stage steps (tools/micro)
+  long long tprof = 0, tsprof = 0;
 #define HTP_PROF(k) do { const long long t_ = c.clock(); pcyc[k] += t_ - tprof; tprof = t_; } while (0)
 #define HTP_PROF0() do { tprof = c.clock(); } while (0)
+#define HTP_SPROF(k) do { const long long t_ = c.clock(); spcyc[k] += t_ - tsprof; tsprof = t_; } while (0)
+#define HTP_SPROF0() do { tsprof = c.clock(); } while (0)
 #else
 #define HTP_PROF(k) do { } while (0)
 #define HTP_PROF0() do { } while (0)
+#define HTP_SPROF(k) do { } while (0)
+#define HTP_SPROF0() do { } while (0)
 #endif
   // filter (wave-uniform): entries live in per-wave LDS (c.lds + FILT_OFF)
   static constexpr int FMAX = 64;
@@ -1365,6 +1387,38 @@ struct ObcaSolver {
   // one per lane, through the Bunch-Kaufman path (local_pivoted).  Before, a 64-block trip holding
   // any pivoted block ran that path for the whole wave -- nearly every trip.  Each block's
   // arithmetic is unchanged, so the results are bit-identical.
+  // block p's right-hand side v (before the solve) and the eliminated rows' q3 (local_rhs_sweep)
+  template <int EN, int EM>
+  HTP_HD HTP_FI void local_rhs_vec(int p, const LocalBlock<EN, EM>& B, const gd* bx, const gd* bs, const gd* bc,
+                                   const gd* bd, double* v, double& q3) const {
+    constexpr int NZ = LocalBlock<EN, EM>::NZ;
+    int i, m, n, mu0, la0;
+    pair_index(p, i, m, n, mu0, la0);
+    const int em = D.eo[m], en = D.eb[n];
+    const int re = D.ePair + 2 * p;
+    const double bd1 = bd[2 * p], bs1 = bs[2 * p], bd3 = bd[2 * p + 1], bs3 = bs[2 * p + 1];
+    const double bc0 = bc[re], bc1 = bc[re + 1];
+    double bxz[NZ];
+    for (int j = 0; j < EN; ++j) bxz[j] = bx[mu0 + (j < en ? j : 0)];
+    for (int j = 0; j < EM; ++j) bxz[EN + j] = bx[la0 + (j < em ? j : 0)];
+    const double q1 = (bd1 + bs1 / B.Ds1) / B.E1;
+    q3 = (bd3 + bs3 / B.Ds3) / B.E3;
+    for (int j = 0; j < EN; ++j) v[j] = (j < en ? bxz[j] : 0.0) + B.J1[j] * q1 + B.J3z[j] * q3;
+    for (int j = 0; j < EM; ++j) v[EN + j] = (j < em ? bxz[EN + j] : 0.0) + B.J1[EN + j] * q1 + B.J3z[EN + j] * q3;
+    v[NZ] = bc0;
+    v[NZ + 1] = bc1;
+  }
+  // block p's stage contribution from its solved v (local_rhs_sweep)
+  template <int EN, int EM>
+  HTP_HD HTP_FI void local_rhs_out(int p, const LocalBlock<EN, EM>& B, const double* v, double q3, gd* PR) const {
+    constexpr int NL = LocalBlock<EN, EM>::NL;
+    for (int col = 0; col < 3; ++col) {
+      double acc = 0.0;
+      for (int r = 0; r < NL; ++r) acc += B.B[r][col] * v[r];
+      PR[3 * p + col] = -acc + (col < 2 ? B.J3p[col] * q3 : 0.0);
+    }
+  }
+
   template <int EN, int EM>
   // inertia of local block p at (dw, dc), exactly as local_factor_sweep decides it (LDL^T, or Bunch-Kaufman when
   // that needs pivoting)
@@ -1407,9 +1461,13 @@ struct ObcaSolver {
       }
       sc_pass = 64;
     };
+#ifdef HTP_LPROF
+    long long lt0 = c.clock(), lscan = 0;
+#endif
     for (int b0 = 0; b0 < D.P; b0 += c.width) {
       const int p = b0 + c.lane;
       bool piv = false;
+      HTP_LP(2, 1);
       if (p < D.P) {
         LocalBlock<EN, EM> B;
         build_local<EN, EM>(B, p, ls, dw, dc);
@@ -1438,7 +1496,19 @@ struct ObcaSolver {
               S[sidx(row, col)] = acc;
             }
           for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
+          if (fuse_rhs) {   // the Newton step's right-hand side (kkt_solve's local_rhs_sweep, fused)
+            double v[NL], q3;
+            local_rhs_vec<EN, EM>(p, B, A(L.xt), A(L.rs), A(L.rc), A(L.rd), v, q3);
+            B.solve(v);
+            local_rhs_out<EN, EM>(p, B, v, q3, A(L.pairR));
+          }
+#ifdef HTP_LPROF
+          const long long ls0 = c.clock();
+#endif
           if (ic_scan) scan(p, nb0, zb0);   // after the block is dead (registers)
+#ifdef HTP_LPROF
+          lscan += c.clock() - ls0;
+#endif
         }
       }
       int cnt;
@@ -1447,17 +1517,27 @@ struct ObcaSolver {
       npiv += cnt;
     }
     c.sync();
+#ifdef HTP_LPROF
+    const long long lt1 = c.clock();
+    HTP_LP(0, lt1 - lt0);
+    HTP_LP(4, (long long)c.maxv((double)lscan));
+    HTP_LP(5, npiv);
+    HTP_LP(6, 1);
+#endif
     for (int b0 = 0; b0 < npiv; b0 += c.width) {
       const int q = b0 + c.lane;
+      HTP_LP(3, 1);
       if (q < npiv) {
         const int p = (int)PL[q];
         LocalBlock<EN, EM> B;
         build_local<EN, EM>(B, p, ls, dw, dc);
-        double Vp[3 * NL];
+        double Vp[4 * NL], q3 = 0.0;
         for (int col = 0; col < 3; ++col)
           for (int r = 0; r < NL; ++r) Vp[col * NL + r] = B.B[r][col];
+        if (fuse_rhs) local_rhs_vec<EN, EM>(p, B, A(L.xt), A(L.rs), A(L.rc), A(L.rd), Vp + 3 * NL, q3);
         int pn[2];
-        local_pivoted<EN, EM>(p, ls, dw, dc, Vp, 3, pn);
+        local_pivoted<EN, EM>(p, ls, dw, dc, Vp, fuse_rhs ? 4 : 3, pn);
+        if (fuse_rhs) local_rhs_out<EN, EM>(p, B, Vp + 3 * NL, q3, A(L.pairR));
         neg += pn[0];
         zero |= pn[1];
         double S[6];
@@ -1471,6 +1551,9 @@ struct ObcaSolver {
         if (ic_scan) scan(p, pn[0], pn[1]);
       }
     }
+#ifdef HTP_LPROF
+    HTP_LP(1, c.clock() - lt1);
+#endif
     if (ic_scan) {   // every trial before min(latest first-right, earliest zero) fails without a zero pivot
       const int pass = (int)c.maxv((double)sc_pass), zr = (int)c.minv((double)sc_zero);
       const int first = pass < zr ? pass : zr;
@@ -1488,32 +1571,12 @@ struct ObcaSolver {
     }
     gd* PR = A(L.pairR);
     gd* PL = A(L.plist);
-    constexpr int NZ = LocalBlock<EN, EM>::NZ;
     constexpr int NL = LocalBlock<EN, EM>::NL;
-    // block p's right-hand side v (before the solve) and the eliminated rows' q3
     auto rhs = [&](int p, const LocalBlock<EN, EM>& B, double* v, double& q3) {
-      int i, m, n, mu0, la0;
-      pair_index(p, i, m, n, mu0, la0);
-      const int em = D.eo[m], en = D.eb[n];
-      const int re = D.ePair + 2 * p;
-      const double bd1 = bd[2 * p], bs1 = bs[2 * p], bd3 = bd[2 * p + 1], bs3 = bs[2 * p + 1];
-      const double bc0 = bc[re], bc1 = bc[re + 1];
-      double bxz[NZ];
-      for (int j = 0; j < EN; ++j) bxz[j] = bx[mu0 + (j < en ? j : 0)];
-      for (int j = 0; j < EM; ++j) bxz[EN + j] = bx[la0 + (j < em ? j : 0)];
-      const double q1 = (bd1 + bs1 / B.Ds1) / B.E1;
-      q3 = (bd3 + bs3 / B.Ds3) / B.E3;
-      for (int j = 0; j < EN; ++j) v[j] = (j < en ? bxz[j] : 0.0) + B.J1[j] * q1 + B.J3z[j] * q3;
-      for (int j = 0; j < EM; ++j) v[EN + j] = (j < em ? bxz[EN + j] : 0.0) + B.J1[EN + j] * q1 + B.J3z[EN + j] * q3;
-      v[NZ] = bc0;
-      v[NZ + 1] = bc1;
+      local_rhs_vec<EN, EM>(p, B, bx, bs, bc, bd, v, q3);
     };
     auto out = [&](int p, const LocalBlock<EN, EM>& B, const double* v, double q3) {
-      for (int col = 0; col < 3; ++col) {
-        double acc = 0.0;
-        for (int r = 0; r < NL; ++r) acc += B.B[r][col] * v[r];
-        PR[3 * p + col] = -acc + (col < 2 ? B.J3p[col] * q3 : 0.0);
-      }
+      local_rhs_out<EN, EM>(p, B, v, q3, PR);
     };
     int npiv = 0;
     for (int b0 = 0; b0 < D.P; b0 += c.width) {
@@ -2649,8 +2712,9 @@ struct ObcaSolver {
   static constexpr int V0 = 8;  // row of v_i in u_i
   // F_i[frow][fcol] (fcol over u_i): stage-independent source of this lane's element
   struct FSrc { int kind, off; };  // 0 zero, 3 J (offset in the LD slot), 4 one
+  template <int NV>
   HTP_HD HTP_FI FSrc f_src(int frow, int fcol) const {
-    const int nv = D.nw - NS;
+    constexpr int nv = NV;
     if (frow < NS) {
       if (fcol < NS) return FSrc{3, JOFF + frow * 8 + fcol};
       if (fcol >= V0 && fcol < V0 + nv) return FSrc{3, JOFF + frow * 8 + NS + (fcol - V0)};
@@ -2663,8 +2727,17 @@ struct ObcaSolver {
     return f.kind == 3 ? slot[f.off] : (f.kind == 4 ? 1.0 : 0.0);
   }
 
+  // The stage chain's v-block width nv = nw - 5 (2: u; 3: u and tau with time-optimal scaling) as a template
+  // argument: every per-lane index test and the 3 x 3 Cholesky unroll at compile time (28 % fewer cycles per
+  // factor stage, tools/micro/ric_micro.hip); the arithmetic is unchanged.
   HTP_HD HTP_FI int riccati_factor_mfma(double dc) {
-    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
+    if constexpr (PT) return riccati_factor_mfma_t<2>(dc);
+    else return D.nw == NS + 3 ? riccati_factor_mfma_t<3>(dc) : riccati_factor_mfma_t<2>(dc);
+  }
+  template <int NV>
+  HTP_HD HTP_FI int riccati_factor_mfma_t(double dc) {
+    constexpr int nv = NV, nz = NS + nv;
+    const int N = D.N, nb = D.nb;
     const int64_t nb2 = (int64_t)nb * nb;
     const int col = c.lane & 15, rg = c.lane >> 4;
     ld* Mv = c.lds;           // 3 x 16: rows v of M
@@ -2681,7 +2754,7 @@ struct ObcaSolver {
       else if (row >= V0 && row - V0 < 2 && col >= NS && col < nz) { hk[r] = 2; ho[r] = (NS + 5 + row - V0) * nb + NS + 5 + (col - NS); }
       else if (col >= V0 && col - V0 < 2 && row >= NS && row < nz) { hk[r] = 2; ho[r] = (NS + 5 + col - V0) * nb + NS + 5 + (row - NS); }
     }
-    for (int sgm = 0; sgm < 2; ++sgm) fs[sgm] = f_src(rg + 4 * sgm, col);
+    for (int sgm = 0; sgm < 2; ++sgm) fs[sgm] = f_src<NV>(rg + 4 * sgm, col);
     const gd* Kst = A(L.Kst);
     const gd* Off = A(L.Off);
     const gd* LDa = A(L.LD);
@@ -2814,7 +2887,13 @@ struct ObcaSolver {
   // forward z_0 = 0.  Per-stage p_i (8 x 5) and rt_i (3 x 5) go to the fac slot after relax_P's T / Q.
   // Records are read straight from HBM one stage ahead.  Result: sig[5 x 5] (global).
   HTP_HD HTP_FI void riccati_sigma_mfma(gd* sig) {
-    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
+    if (D.nw == NS + 3) riccati_sigma_mfma_t<3>(sig);
+    else riccati_sigma_mfma_t<2>(sig);
+  }
+  template <int NV>
+  HTP_HD HTP_FI void riccati_sigma_mfma_t(gd* sig) {
+    constexpr int nv = NV, nz = NS + nv;
+    const int N = D.N, nb = D.nb;
     const int64_t nb2 = (int64_t)nb * nb;
     const int col = c.lane & 15, rg = c.lane >> 4;
     const bool cw = col < NS;                 // a right-hand-side column
@@ -2822,8 +2901,8 @@ struct ObcaSolver {
     gd* Fa = A(L.fac);
     constexpr int PO = 50, RO = 90;           // p_i [8][5] and rt_i [3][5] in fac slot i
     FSrc fT[2], fA[3];
-    for (int sgm = 0; sgm < 2; ++sgm) fT[sgm] = f_src(rg + 4 * sgm, col);
-    for (int sgm = 0; sgm < 3; ++sgm) fA[sgm] = f_src(col, rg + 4 * sgm);
+    for (int sgm = 0; sgm < 2; ++sgm) fT[sgm] = f_src<NV>(rg + 4 * sgm, col);
+    for (int sgm = 0; sgm < 3; ++sgm) fA[sgm] = f_src<NV>(col, rg + 4 * sgm);
     auto p_at = [&](const gd* slot, int sgm) {
       const int k = rg + 4 * sgm;
       return (col < nz && k < nz) ? (double)slot[col * 8 + k] : 0.0;
@@ -2949,6 +3028,39 @@ struct ObcaSolver {
   HTP_HD HTP_FI void ring_fill(ld* ring, int lo, int cnt, const gd* V, const gd* X) {
     const int N = D.N, nb = D.nb;
     const int64_t nb2 = (int64_t)nb * nb;
+#if HTP_RING_FILL_LANE
+    // Lane l copies elements k = l + 64 j (j < 4) of every stage record; where element k comes from (LD slot,
+    // V_i, X_i or the T / Q records in fac) does not depend on the stage, so the four sources are resolved once
+    // and each load is base + stage * stride.  Same values as the element-major copy below.
+    constexpr int J = (RS_L + 63) / 64;
+    const gd* src[J];
+    int64_t strd[J];
+    bool ok[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int k = c.lane + 64 * j;
+      if (k < RS_SLOT) { src[j] = A(L.LD) + k; strd[j] = nb2; ok[j] = true; }
+      else if (k < RS_X) { src[j] = V + (k - RS_V); strd[j] = nb; ok[j] = k - RS_V < nb; }
+      else if (k < RS_T) { src[j] = X + (k - RS_X); strd[j] = nb; ok[j] = k - RS_X < nb; }
+      else { src[j] = A(L.fac) + (k < RS_L ? k - RS_T : 0); strd[j] = nb2; ok[j] = k < RS_L && ric_relax; }
+    }
+    double v[RING_SB + 1][J];
+#pragma unroll
+    for (int sb = 0; sb <= RING_SB; ++sb) {               // every load of the block issues first
+      const int st = lo + sb;
+      const bool in = sb < cnt && st < N;
+      const int64_t stc = in ? st : 0;
+#pragma unroll
+      for (int j = 0; j < J; ++j) v[sb][j] = (in && ok[j]) ? (double)src[j][stc * strd[j]] : 0.0;
+    }
+#pragma unroll
+    for (int sb = 0; sb <= RING_SB; ++sb)
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int k = c.lane + 64 * j;
+        if (sb < cnt && k < RS_L) ring[sb * RS_L + k] = v[sb][j];
+      }
+#else
     const gd* LDa = A(L.LD);
     const gd* Fa = A(L.fac);
     const int tot = cnt * RS_L;
@@ -2970,20 +3082,28 @@ struct ObcaSolver {
       const int e = c.lane + u * c.width;
       if (e < tot) ring[e] = v[u];
     }
+#endif
   }
 
   HTP_HD HTP_FI void riccati_solve_mfma(const gd* V, gd* X) {
+    if constexpr (PT) riccati_solve_mfma_t<2>(V, X);
+    else if (D.nw == NS + 3) riccati_solve_mfma_t<3>(V, X);
+    else riccati_solve_mfma_t<2>(V, X);
+  }
+  template <int NV>
+  HTP_HD HTP_FI void riccati_solve_mfma_t(const gd* V, gd* X) {
 #if defined(HTP_KKT_PROF) && HTP_KKT_PROF == 2
     long long kt_ric = c.clock();
 #endif
-    const int N = D.N, nb = D.nb, nv = D.nw - NS, nz = NS + nv;
+    constexpr int nv = NV, nz = NS + nv;
+    const int N = D.N, nb = D.nb;
     const int col = c.lane & 15, rg = c.lane >> 4;
     const bool c0 = col == 0;
     ld* ring = c.lds + RING_OFF;
     // per-lane record maps: F rows as B / F' as A (2), F as A (3), P as A (2), K' as A (1), K at rows V0.. as A (2)
     FSrc fT[2], fA[3];
-    for (int sgm = 0; sgm < 2; ++sgm) fT[sgm] = f_src(rg + 4 * sgm, col);
-    for (int sgm = 0; sgm < 3; ++sgm) fA[sgm] = f_src(col, rg + 4 * sgm);
+    for (int sgm = 0; sgm < 2; ++sgm) fT[sgm] = f_src<NV>(rg + 4 * sgm, col);
+    for (int sgm = 0; sgm < 3; ++sgm) fA[sgm] = f_src<NV>(col, rg + 4 * sgm);
     auto p_at = [&](const ld* slot, int sgm) {  // P[col][4 sgm + rg] (P symmetric, 8 x 8 stride 8)
       const int k = rg + 4 * sgm;
       return (col < nz && k < nz) ? (double)slot[col * 8 + k] : 0.0;
@@ -3041,9 +3161,11 @@ struct ObcaSolver {
     for (int hi = N - 2; hi >= 0; hi -= RING_SB) {
       lo = hi - RING_SB + 1 > 0 ? hi - RING_SB + 1 : 0;
       c.sync();                                       // the previous block's LDS reads are done
+      HTP_SPROF0();
       ring_fill(ring, lo, hi - lo + 2, V, X);         // stages lo .. hi + 1
       c.sync();
       ld_b(hi, bc);
+      HTP_SPROF(0);
       for (int i = hi; i >= lo; --i) {
         if (i > lo) ld_b(i - 1, bn);
         dbl4 w = Ctx::mfma16(bc.mp[0], bc.e[0], pv);          // w = p - P e
@@ -3069,6 +3191,7 @@ struct ObcaSolver {
         }
         if (c0 && rg < nv) Xi[nz + rg] = g[2];
         bc = bn;
+        HTP_SPROF(1);
       }
     }
     c.sync();
@@ -3108,9 +3231,11 @@ struct ObcaSolver {
     for (lo = 0; lo < N; lo += RING_SB) {
       const int hi = lo + RING_SB - 1 < N - 1 ? lo + RING_SB - 1 : N - 1;
       c.sync();
+      HTP_SPROF0();
       ring_fill(ring, lo, hi - lo + 2, V, X);         // stages lo .. hi + 1 (X_i holds p_i, rt_i here)
       c.sync();
       ld_f(lo, fc);
+      HTP_SPROF(2);
       for (int i = lo; i <= hi; ++i) {
         if (i < hi) ld_f(i + 1, fn);
         dbl4 y = {fc.p[0], fc.p[1], 0.0, 0.0};                 // y = p - P z
@@ -3150,6 +3275,7 @@ struct ObcaSolver {
           if (c0 && row < NS) Xi[NS + row] = r == 0 ? zr0 : zr1;
         }
         fc = fn;
+        HTP_SPROF(3);
       }
     }
     c.sync();
@@ -3634,7 +3760,8 @@ struct ObcaSolver {
   }
 
   HTP_HD HTP_PHASE void kkt_solve(bool ls, double dw, double dc, const gd* bx, const gd* bs, const gd* bc,
-                        const gd* bd, gd* ox, gd* os, gd* oc, gd* od, const gd* bR = nullptr, gd* oR = nullptr) {
+                        const gd* bd, gd* ox, gd* os, gd* oc, gd* od, const gd* bR = nullptr, gd* oR = nullptr,
+                        bool rhs_done = false) {
     const int N = D.N, nb = D.nb;
     const long long t0 = c.clock();
     if (rs) {  // fold the n/p right-hand sides into the constraint rows
@@ -3659,7 +3786,7 @@ struct ObcaSolver {
 #ifdef HTP_KKT_PROF
     long long tk = c.clock();
 #endif
-    local_rhs_sweep<EN_, EM_>(ls, dw, dc, bx, bs, bc, bd);
+    if (!rhs_done) local_rhs_sweep<EN_, EM_>(ls, dw, dc, bx, bs, bc, bd);   // else: pairR from the factor sweep
     c.sync();
     HTP_KPROF(0, tk);
 #if defined(HTP_KKT_PROF) && HTP_KKT_PROF == 2
@@ -4430,6 +4557,10 @@ struct ObcaSolver {
       for (int k = 0; k < 8; ++k)
         if (k != 4) res.cyc[k] = pcyc[k];
 #endif
+#ifdef HTP_LPROF
+      { const int slot[7] = {0, 1, 2, 3, 5, 6, 7};
+        for (int k = 0; k < 7; ++k) res.cyc[slot[k]] = lprof[k]; }
+#endif
 #ifdef HTP_KKT_PROF
 #if HTP_KKT_PROF == 2
       const int slot[7] = {0, 1, 2, 3, 5, 6, 7};
@@ -5152,13 +5283,16 @@ struct ObcaSolver {
       // Newton step: rx (in xt), rs, rc, rd[, rRx]; barrier gradient in sx, ss
       build_newton_rhs(gl);
       double dw = 0.0, dc = 0.0;
+      fuse_rhs = HTP_FUSE_RHS && !PT && !rs;   // restoration folds its n/p rows into the rhs per trial: unfused
       const bool have_step = factor_ic(dw, dc);
+      const bool rhs_done = fuse_rhs;
+      fuse_rhs = false;
       if (!have_step) {
         ls_.fallback = 1;
       } else {
         if (dw > 0.0) dw_last = dw;
         HTP_TRACE("[trace] factored dw=%g\n", dw);
-        kkt_solve(false, dw, dc, A(L.xt), A(L.rs), A(L.rc), A(L.rd), dx, ds, dyc, dyd, A(L.rRx), dR);
+        kkt_solve(false, dw, dc, A(L.xt), A(L.rs), A(L.rc), A(L.rd), dx, ds, dyc, dyd, A(L.rRx), dR, rhs_done);
       }
       // ---- line search (IpBacktrackingLineSearch::FindAcceptableTrialPoint)
       long long tls = c.clock();

@@ -13,6 +13,12 @@ instance, with the transcendental functions taken from glibc (CPython's math mod
 SX VM calls in the reference's own solve) instead of numpy's AVX-512 kernels:
 
     python tests/golden/make_witness.py E12:glibc E54:glibc  -> tests/golden/witness/<name>_libm.npz
+
+Input-rounding witnesses: the same oracle on the fixture's instance with ONE input double moved by one ulp
+(the first initial-guess state x_0 component K, np.nextafter), i.e. an instance the reference cannot tell
+apart from the fixture's after its own float parsing and arithmetic:
+
+    python tests/golden/make_witness.py E12:ulp0 E12:ulp1   -> tests/golden/witness/<name>_ulp<K>.npz
 """
 import os
 import sys
@@ -31,6 +37,8 @@ def run(name):
     t = time.time()
     if name.endswith(":glibc"):
         return run_libm(name.split(":")[0], t)
+    if ":ulp" in name:
+        return run_ulp(name.split(":")[0], int(name.split(":ulp")[1]), t)
     if name.startswith("P"):   # point formulation, tests/test_gpu_points.py small instances (N=12, M=2)
         from headland_trajectory_planning_amd import synth
         from oracle.nlp_points import PointNLP
@@ -84,6 +92,32 @@ def run_libm(name, t):
              seconds=time.time() - t)
     d = float(np.max(np.abs(a["x"][:5 * N] - b["x"][:5 * N])))
     return (f"{name} libm: numpy status {a['status']} it {a['iters']} resto {a['n_resto']} | glibc status "
+            f"{b['status']} it {b['iters']} resto {b['n_resto']} | max state diff {d:.3g} ({time.time() - t:.0f} s)")
+
+
+def run_ulp(name, k, t):
+    from _fixture_io import load_instance
+    from oracle.ipm import IpoptRestatement
+    from oracle.nlp import ObcaNLP
+    from oracle.structured import StructuredKKT
+    g = np.load(os.path.join(ROOT, "tests", "golden", "obca_full", f"{name}.npz"))
+    inst = load_instance(g)
+    tr = np.array(inst["init_traj"], dtype=np.float64)
+    row, col = (k // 2, (k % 2)) if k < 4 else (1 + k, 0)
+    tr[row, col] = np.nextafter(tr[row, col], np.inf)
+    inst = dict(inst, init_traj=tr)
+    nlp = ObcaNLP(inst)
+    N = int(g["N"])
+    a = {"x": g["states"], "status": int(g["status"]), "iters": int(g["iters"]), "n_resto": int(g["n_resto"])}
+    b = IpoptRestatement(nlp, kkt=StructuredKKT(nlp)).solve()
+    orders = ("StructuredKKT", f"StructuredKKT, init_traj[{row},{col}] + 1 ulp")
+    os.makedirs(OUT, exist_ok=True)
+    np.savez(os.path.join(OUT, f"{name}_ulp{k}.npz"), orders=np.array(orders),
+             states_a=a["x"][:5 * N], status_a=a["status"], iters_a=a["iters"], n_resto_a=a["n_resto"],
+             states_b=b["x"][:5 * N], status_b=b["status"], iters_b=b["iters"], n_resto_b=b["n_resto"],
+             seconds=time.time() - t)
+    d = float(np.max(np.abs(a["x"][:5 * N] - b["x"][:5 * N])))
+    return (f"{name} ulp{k}: fixture status {a['status']} it {a['iters']} resto {a['n_resto']} | +1 ulp status "
             f"{b['status']} it {b['iters']} resto {b['n_resto']} | max state diff {d:.3g} ({time.time() - t:.0f} s)")
 
 

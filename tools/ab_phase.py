@@ -39,6 +39,13 @@ for rnd in range(2):
             if "kp2" in k:   # HTP_KKT_PROF=2: rhs sweep, stage rhs, Riccati backward, forward, ric+scatter, back sweep, n_kkt
                 nm = ["rhs_sweep", "stage_rhs", "ric_bwd", "ric_fwd", "total", "ric+scatter", "back_sweep", "n_kkt"]
                 line += " | kkt solves per iteration %.3f" % (cyc[:, 7].sum() / max(1, r.iterations.sum()))
+            if "lp" in k.split("_")[0] and "prof" not in k:   # HTP_LPROF: local factor sweep
+                nm = ["pass1_cyc", "pass2_cyc", "pass1_trips", "pass2_trips", "total", "scan_cyc", "n_piv", "n_sweeps"]
+                sw = max(1.0, cyc[:, 7].sum())
+                line += " | per sweep: pass1 %.0f cyc (%.2f trips), pass2 %.0f cyc (%.2f trips), scan %.0f cyc, %.1f " \
+                        "pivoted blocks; sweeps per iteration %.2f" % (cyc[:, 0].sum() / sw, cyc[:, 2].sum() / sw,
+                        cyc[:, 1].sum() / sw, cyc[:, 3].sum() / sw, cyc[:, 5].sum() / sw, cyc[:, 6].sum() / sw,
+                        sw / max(1, r.iterations.sum()))
             if "prof" in k and "kprof" not in k:   # HTP_PROF_ON: stage-chain sub-steps (factor 1/3/5, solve 6/7)
                 nm = ["p0", "fac_mfma", "p2", "fac_chol", "total", "fac_tail", "solve_bwd*", "solve_fwd"]
             line += " | " + " ".join(f"{nm[j]} {cyc[:, j].sum() / tot:.3f}" for j in (0, 1, 2, 3, 5, 6, 7))

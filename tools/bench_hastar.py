@@ -24,8 +24,12 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--max-nodes", type=int, default=400)
-    ap.add_argument("--cpu-sample", type=int, default=64)
+    ap.add_argument("--cpu-sample", type=int, default=512)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiled runs)")
+    ap.add_argument("--lib", default="", help="A/B: libhtp_<name>.so instead of libhtp.so")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (libhtp_cpu.so htp_cpu_hastar_range, OpenMP); 0 = OMP_NUM_THREADS or "
+                         "the affinity mask")
     args = ap.parse_args()
     import torch
 
@@ -37,7 +41,8 @@ def main():
     # only searches whose start and goal poses are collision free: a blocked pair ends before any
     # expansion (HTP_HA_START_GOAL_BLOCKED) and would inflate searches/s.  Seeds are screened with a
     # 1-node search on the GPU (the blocked test runs before the first expansion), outside the timing.
-    ctx = _native.Context(0)
+    lib = _native.load(_native.LIB_PATH.replace("libhtp.so", f"libhtp_{args.lib}.so")) if args.lib else None
+    ctx = _native.Context(0, lib=lib) if lib else _native.Context(0)
     want = min(args.batch, 512)
     uniq, seed, skipped = [], 0, 0
     while len(uniq) < want:
@@ -81,11 +86,44 @@ def main():
     ne = int(out["n_expanded"].sum().item())
     npose = int(out["n_pose"].sum().item())
     kms = float(np.mean(ms))
-    # CPU baseline: serial host build of the same core on the first problems
+    # CPU baseline: libhtp_cpu.so's OpenMP build of the same core (htp_cpu_hastar_range: one search per thread,
+    # g++ -O3 -march=x86-64-v3, fp-contract off) on the first problems, bounded by --cpu-sample
     n = 0 if args.no_cpu else min(args.cpu_sample, B)
-    t = time.perf_counter()
-    hres = H.hastar_host(probs[:n]) if n else None
-    cpu_s = time.perf_counter() - t
+    cpu = None
+    if n:
+        import ctypes
+        try:
+            affinity = len(os.sched_getaffinity(0))
+        except AttributeError:
+            affinity = os.cpu_count() or 1
+        cap = os.environ.get("OMP_NUM_THREADS")
+        threads = args.cpu_threads or (min(affinity, int(cap)) if cap else affinity)
+        cl = ctypes.CDLL(_native.CPU_LIB_PATH)
+        cl.htp_cpu_hastar_range.argtypes = [ctypes.POINTER(_native.HaBatch), ctypes.POINTER(_native.HaResult),
+                                            ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
+        cl.htp_cpu_hastar_range.restype = ctypes.c_int
+        cpk = _native.HastarPacked(probs[:n], cap_path=4096, cap_log=0)
+        cres = _native.HastarResults(cpk)
+        t = time.perf_counter()
+        assert cl.htp_cpu_hastar_range(ctypes.byref(cpk.struct()), ctypes.byref(cres.struct()), 0, n, threads) == 0
+        cpu_s = time.perf_counter() - t
+        same = bool(np.array_equal(cres.status, st[:n]) and np.array_equal(cres.counter, out["counter"].cpu().numpy()[:n]))
+        cpu = {"value": n / cpu_s, "unit": "searches/s", "cores": threads, "kind": "port",
+               "sample": f"first {n} searches of the same batch, libhtp_cpu.so htp_cpu_hastar_range (csrc/hastar_core.h, "
+                         f"g++ -O3 -march=x86-64-v3 -fopenmp, {threads} threads, one search per thread) in {cpu_s:.1f} s",
+               "pose_tests_per_s": float(np.asarray(cres.n_pose).sum()) / cpu_s, "nproc": os.cpu_count(),
+               "affinity_cores": affinity, "same_status_and_counter_as_gpu": same,
+               "cores_note": "explicit cap = OMP_NUM_THREADS (the job's CPU share on the GPU pool)" if cap else
+                             "every CPU in the affinity mask"}
+    import hashlib
+    hh = hashlib.sha256()
+    for k in ("status", "counter", "n_path", "n_expanded", "n_pose"):
+        hh.update(out[k].cpu().numpy().tobytes())
+    npth = out["n_path"].cpu().numpy()
+    for k in ("x", "y", "yaw"):
+        a = out[k].cpu().numpy()
+        for b in range(B):
+            hh.update(a[b, :max(0, min(int(npth[b]), pk.cap_path))].tobytes())
     line = {"metric": "hybrid A* headland searches/s (King, res 0.2, max_nodes %d)" % args.max_nodes,
             "value": B / (kms / 1e3), "unit": "searches/s", "batch": B, "kernel_ms": kms, "wall_ms": wall * 1e3,
             "pose_tests_per_s": npose / (kms / 1e3), "expansions_per_s": ne / (kms / 1e3),
@@ -93,11 +131,8 @@ def main():
             "expanding_searches_per_s": float(np.sum(out["n_expanded"].cpu().numpy() > 0)) / (kms / 1e3),
             "workload": f"{len(uniq)} unique collision-free start/goal scenarios (tests/_ha_util.scenario, "
                         f"{skipped} blocked seeds skipped) repeated to {B}",
-            "gen_s": gen_s,
-            "cpu_baseline": None if not n else
-                            {"value": n / cpu_s, "unit": "searches/s", "cores": 1, "kind": "port",
-                             "sample": f"first {n} searches, serial host build of csrc/hastar_core.h (g++ -O2)",
-                             "pose_tests_per_s": float(hres.n_pose.sum()) / cpu_s}}
+            "gen_s": gen_s, "out_sha16": hh.hexdigest()[:16], "lib": args.lib or "libhtp.so",
+            "cpu_baseline": cpu}
     print(json.dumps(line))
 
 
