@@ -48,10 +48,10 @@ HTP_HD inline double estrin7(const double* c, double z, double z2, double z4) {
 // inline into the solver's loops without the double-double code (the compiler would otherwise outline the whole
 // function, and every call site pays the caller-saved register spills of a 512-register kernel).
 #if defined(__GNUC__) || defined(__clang__)
-#define HTP_FM_NOINLINE __attribute__((noinline))
+#define HTP_FM_NOINLINE __attribute__((noinline)) inline
 #define HTP_FM_INLINE __attribute__((always_inline)) inline
 #else
-#define HTP_FM_NOINLINE
+#define HTP_FM_NOINLINE inline
 #define HTP_FM_INLINE inline
 #endif
 struct SinCos { double s, c; };

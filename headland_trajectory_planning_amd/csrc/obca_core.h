@@ -396,6 +396,196 @@ HTP_HD inline void bk_solve_packed(T* K, const int* ip, int n, double* v) {
   }
 }
 
+// The same Bunch-Kaufman factorization and solves for a compile-time n, written for SIMD execution: the lanes of
+// a wavefront each factor their own block with their own pivots, so every loop runs over the full compile-time
+// range with per-lane predicates (no lane-dependent trip counts or divergent loop control); element (r, q) of the
+// packed block sits at K[S (r (r + 1) / 2 + q)] (S = 64: the lanes' blocks interleaved in LDS, a constant offset
+// from the lane's base for constant r, q); the pivot vector and the right-hand sides live in registers (constant
+// indices; the per-lane k / kp are reached through selects).  Every element sees the operations of
+// bk_factor_packed / bk_solve_packed above in the same order, so factors, inertia and solutions are bit-identical.
+template <int S, class T>
+HTP_HD HTP_FI inline T& pkx(T* K, int r, int c) { return K[S * (r >= c ? r * (r + 1) / 2 + c : c * (c + 1) / 2 + r)]; }
+template <int n, class V>
+HTP_HD HTP_FI inline V sel_get(const V* v, int k) {
+  V r = v[0];
+#pragma unroll
+  for (int j = 1; j < n; ++j) r = (k == j) ? v[j] : r;
+  return r;
+}
+template <int n>
+HTP_HD HTP_FI inline void sel_set(double* v, int k, double x) {
+#pragma unroll
+  for (int j = 0; j < n; ++j) v[j] = (k == j) ? x : v[j];
+}
+
+template <int n, int S, class T>
+HTP_HD HTP_FI inline void bk_factor_simd(T* K, int* ip, int& neg, int& zero) {
+  const double alpha = 0.6403882032022076;
+  neg = 0;
+  zero = 0;
+#pragma unroll
+  for (int j = 0; j < n; ++j) ip[j] = 0;
+  int k = 0;
+#pragma unroll 1
+  for (int step = 0; step < n; ++step) {
+    const bool act = k < n;
+    const int kc = act ? k : 0;                    // a valid index for the finished lanes' (unused) loads
+    int kstep = 1, kp = kc;
+    const double absakk = fabs((double)K[S * (kc * (kc + 1) / 2 + kc)]);
+    int imax = kc;
+    double colmax = 0.0;
+#pragma unroll
+    for (int r = 1; r < n; ++r)
+      if (r > kc) {
+        const double v = fabs((double)K[S * (r * (r + 1) / 2 + kc)]);
+        if (v > colmax) { colmax = v; imax = r; }
+      }
+    if (act && !(absakk >= alpha * colmax) && !(absakk == 0.0 && colmax == 0.0)) {
+      double rowmax = 0.0;
+#pragma unroll
+      for (int j = 0; j < n; ++j)
+        if (j >= kc && j != imax) {
+          const double v = fabs((double)pkx<S>(K, imax, j));
+          if (v > rowmax) rowmax = v;
+        }
+      if (absakk >= alpha * colmax * (colmax / rowmax)) kp = kc;
+      else if (fabs((double)K[S * (imax * (imax + 1) / 2 + imax)]) >= alpha * rowmax) kp = imax;
+      else { kp = imax; kstep = 2; }
+    }
+    const int kk = kc + kstep - 1;
+    if (act && kp != kk) {
+#pragma unroll
+      for (int j = 0; j < n; ++j)
+        if (j >= kc && j != kk && j != kp) {
+          T& a = pkx<S>(K, kk, j);
+          T& b = pkx<S>(K, kp, j);
+          const double t = a; a = b; b = t;
+        }
+      T& a = K[S * (kk * (kk + 1) / 2 + kk)];
+      T& b = K[S * (kp * (kp + 1) / 2 + kp)];
+      const double t = a; a = b; b = t;
+    }
+    if (act && kstep == 1) {
+      double d = K[S * (kc * (kc + 1) / 2 + kc)];
+      if (d == 0.0) { zero = 1; d = 1.0; K[S * (kc * (kc + 1) / 2 + kc)] = 1.0; }
+      if (d < 0.0) ++neg;
+      const double id = 1.0 / d;
+      double lr[n];
+#pragma unroll
+      for (int r = 0; r < n; ++r) lr[r] = (r > kc) ? (double)K[S * (r * (r + 1) / 2 + kc)] * id : 0.0;
+#pragma unroll
+      for (int r = 1; r < n; ++r)
+#pragma unroll
+        for (int q = 1; q <= r; ++q)
+          if (q > kc) K[S * (r * (r + 1) / 2 + q)] -= lr[r] * K[S * (q * (q + 1) / 2 + kc)];
+#pragma unroll
+      for (int r = 1; r < n; ++r)
+        if (r > kc) K[S * (r * (r + 1) / 2 + kc)] *= id;
+#pragma unroll
+      for (int j = 0; j < n; ++j)
+        if (j == kc) ip[j] = kp;
+    } else if (act) {
+      const double d11 = K[S * (kc * (kc + 1) / 2 + kc)], d21 = K[S * ((kc + 1) * (kc + 2) / 2 + kc)];
+      const double d22 = K[S * ((kc + 1) * (kc + 2) / 2 + kc + 1)];
+      const double det = d11 * d22 - d21 * d21;
+      if (det < 0.0) neg += 1;
+      else if (det > 0.0) neg += (d11 + d22 < 0.0) ? 2 : 0;
+      else zero = 1;
+      const double i11 = d22 / det, i22 = d11 / det, i21 = -d21 / det;
+#pragma unroll
+      for (int r = n - 1; r >= 2; --r) {  // descending: rows q < r still hold their original columns
+        if (r >= kc + 2) {
+          const double a1 = K[S * (r * (r + 1) / 2 + kc)], a2 = K[S * (r * (r + 1) / 2 + kc + 1)];
+          const double l1 = a1 * i11 + a2 * i21, l2 = a1 * i21 + a2 * i22;
+#pragma unroll
+          for (int q = 2; q <= r; ++q)
+            if (q >= kc + 2)
+              K[S * (r * (r + 1) / 2 + q)] -= l1 * K[S * (q * (q + 1) / 2 + kc)] + l2 * K[S * (q * (q + 1) / 2 + kc + 1)];
+          K[S * (r * (r + 1) / 2 + kc)] = l1;
+          K[S * (r * (r + 1) / 2 + kc + 1)] = l2;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < n; ++j)
+        if (j == kc || j == kc + 1) ip[j] = -(kp + 1);
+    }
+    k += act ? kstep : 0;
+  }
+}
+
+template <int n, int S, class T>
+HTP_HD HTP_FI inline void bk_solve_simd(T* K, const int* ip, double* v) {
+  int k = 0;
+#pragma unroll 1
+  for (int step = 0; step < n; ++step) {          // forward: P, L, D
+    const bool act = k < n;
+    const int kc = act ? k : 0;
+    const int ipk = sel_get<n>(ip, kc);
+    if (act && ipk >= 0) {
+      const int kp = ipk;
+      if (kp != kc) { const double a = sel_get<n>(v, kc), b = sel_get<n>(v, kp); sel_set<n>(v, kc, b); sel_set<n>(v, kp, a); }
+      const double vk = sel_get<n>(v, kc);
+#pragma unroll
+      for (int r = 1; r < n; ++r)
+        if (r > kc) v[r] -= K[S * (r * (r + 1) / 2 + kc)] * vk;
+      const double dkk = K[S * (kc * (kc + 1) / 2 + kc)];
+#pragma unroll
+      for (int j = 0; j < n; ++j)
+        if (j == kc) v[j] /= dkk;
+      k += 1;
+    } else if (act) {
+      const int kp = -ipk - 1;
+      if (kp != kc + 1) {
+        const double a = sel_get<n>(v, kc + 1), b = sel_get<n>(v, kp);
+        sel_set<n>(v, kc + 1, b);
+        sel_set<n>(v, kp, a);
+      }
+      const double vk = sel_get<n>(v, kc), vk1 = sel_get<n>(v, kc + 1);
+#pragma unroll
+      for (int r = 2; r < n; ++r)
+        if (r > kc + 1) v[r] -= K[S * (r * (r + 1) / 2 + kc)] * vk + K[S * (r * (r + 1) / 2 + kc + 1)] * vk1;
+      const double d11 = K[S * (kc * (kc + 1) / 2 + kc)], d21 = K[S * ((kc + 1) * (kc + 2) / 2 + kc)];
+      const double d22 = K[S * ((kc + 1) * (kc + 2) / 2 + kc + 1)];
+      const double det = d11 * d22 - d21 * d21;
+      const double b1 = vk, b2 = vk1;
+      sel_set<n>(v, kc, (d22 * b1 - d21 * b2) / det);
+      sel_set<n>(v, kc + 1, (-d21 * b1 + d11 * b2) / det);
+      k += 2;
+    }
+  }
+  k = n - 1;
+#pragma unroll 1
+  for (int step = 0; step < n; ++step) {          // backward: L', P'
+    const bool act = k >= 0;
+    const int kc = act ? k : 0;
+    const int ipk = sel_get<n>(ip, kc);
+    if (act && ipk >= 0) {
+      double t = sel_get<n>(v, kc);
+#pragma unroll
+      for (int r = 1; r < n; ++r)
+        if (r > kc) t -= K[S * (r * (r + 1) / 2 + kc)] * v[r];
+      sel_set<n>(v, kc, t);
+      const int kp = ipk;
+      if (kp != kc) { const double a = sel_get<n>(v, kc), b = sel_get<n>(v, kp); sel_set<n>(v, kc, b); sel_set<n>(v, kp, a); }
+      k -= 1;
+    } else if (act) {
+      const int km = kc >= 1 ? kc - 1 : 0;
+      double t = sel_get<n>(v, kc), t1 = sel_get<n>(v, km);
+#pragma unroll
+      for (int r = 1; r < n; ++r)
+        if (r > kc) {
+          t -= K[S * (r * (r + 1) / 2 + kc)] * v[r];
+          t1 -= K[S * (r * (r + 1) / 2 + km)] * v[r];
+        }
+      sel_set<n>(v, kc, t);
+      sel_set<n>(v, km, t1);
+      const int kp = -ipk - 1;
+      if (kp != kc) { const double a = sel_get<n>(v, kc), b = sel_get<n>(v, kp); sel_set<n>(v, kc, b); sel_set<n>(v, kp, a); }
+      k -= 2;
+    }
+  }
+}
+
 // LDS ring of the matrix-core Riccati passes (ObcaSolver::ring_fill): RING_SB + 1 stage records of
 // RS_L doubles (LD slot prefix [0, SOFF + NS), V_i, X_i) after the per-wave scratch and filter.
 #ifndef HTP_RING_SB
@@ -415,6 +605,10 @@ constexpr int RING_OFF = 4 * NBMAX * NBMAX + 8 + 2 * 64;
 constexpr int RING_DOUBLES = (RING_SB + 1) * RS_L;
 // pivoted local blocks (ObcaSolver::local_pivoted) on the device: one packed 10x10 block per lane in LDS,
 // over the same region as the ring (never live at the same time)
+// the pivoted local blocks through the SIMD-convergent Bunch-Kaufman (1) or the per-lane serial one (0, round 4)
+#ifndef HTP_BK_SIMD
+#define HTP_BK_SIMD 1
+#endif
 #ifndef HTP_PIV_LDS
 #define HTP_PIV_LDS 1   // 0: pivoted blocks in private memory (smaller LDS footprint; experiments)
 #endif
@@ -1336,6 +1530,32 @@ struct ObcaSolver {
     for (int k = 0; k < nrhs; ++k) bk_solve_packed(B.K, ip, NL, V + k * NL);
   }
 
+  // local_pivoted as SIMD-convergent code (bk_factor_simd / bk_solve_simd), inlined so that the NRHS right-hand
+  // sides V[c * NL + r] stay in registers; on the device the block goes to this lane's interleaved slice of the
+  // LDS ring region (element e at lds[RING_OFF + 64 e + lane]).  Bit-identical to local_pivoted.
+  template <int EN, int EM, int NRHS>
+  HTP_HD HTP_FI void local_pivoted_v(int p, bool ls, double dw, double dc, double* V, int* inertia) const {
+    constexpr int NL = LocalBlock<EN, EM>::NL;
+    constexpr int NPK = LocalBlock<EN, EM>::NPK;
+    LocalBlock<EN, EM> B;
+    build_local<EN, EM>(B, p, ls, dw, dc);
+    int ip[NL];
+#if defined(__HIPCC__) || defined(HTP_EMU_WAVE)
+    if constexpr (Ctx::kMfma && HTP_PIV_LDS && NPK <= PIV_LDS_PER_LANE) {
+      ld* K = c.lds + RING_OFF + c.lane;
+#pragma unroll
+      for (int q = 0; q < NPK; ++q) K[64 * q] = B.K[q];
+      bk_factor_simd<NL, 64>(K, ip, inertia[0], inertia[1]);
+#pragma unroll
+      for (int k = 0; k < NRHS; ++k) bk_solve_simd<NL, 64>(K, ip, V + k * NL);
+      return;
+    }
+#endif
+    bk_factor_simd<NL, 1>(B.K, ip, inertia[0], inertia[1]);
+#pragma unroll
+    for (int k = 0; k < NRHS; ++k) bk_solve_simd<NL, 1>(B.K, ip, V + k * NL);
+  }
+
   // LocalStore record of block p (HTP_STORE_LOCAL): written by the factor sweep, read by the solve sweeps
   template <int EN, int EM>
   HTP_HD HTP_FI void store_local(const LocalBlock<EN, EM>& B, int p, bool piv) {
@@ -1428,7 +1648,11 @@ struct ObcaSolver {
     B.factor();
     if (!B.piv) { nb = B.neg; zb = B.zero ? 1 : 0; return; }
     int pn[2];
+#if HTP_BK_SIMD
+    local_pivoted_v<EN, EM, 0>(p, ls, dw, dc, nullptr, pn);
+#else
     local_pivoted<EN, EM>(p, ls, dw, dc, nullptr, 0, pn);
+#endif
     nb = pn[0];
     zb = pn[1] ? 1 : 0;
   }
@@ -1536,7 +1760,12 @@ struct ObcaSolver {
           for (int r = 0; r < NL; ++r) Vp[col * NL + r] = B.B[r][col];
         if (fuse_rhs) local_rhs_vec<EN, EM>(p, B, A(L.xt), A(L.rs), A(L.rc), A(L.rd), Vp + 3 * NL, q3);
         int pn[2];
+#if HTP_BK_SIMD
+        if (fuse_rhs) local_pivoted_v<EN, EM, 4>(p, ls, dw, dc, Vp, pn);
+        else local_pivoted_v<EN, EM, 3>(p, ls, dw, dc, Vp, pn);
+#else
         local_pivoted<EN, EM>(p, ls, dw, dc, Vp, fuse_rhs ? 4 : 3, pn);
+#endif
         if (fuse_rhs) local_rhs_out<EN, EM>(p, B, Vp + 3 * NL, q3, A(L.pairR));
         neg += pn[0];
         zero |= pn[1];
@@ -1613,7 +1842,11 @@ struct ObcaSolver {
         double v[NL], q3;
         rhs(p, B, v, q3);
         int pn[2];
+#if HTP_BK_SIMD
+        local_pivoted_v<EN, EM, 1>(p, ls, dw, dc, v, pn);
+#else
         local_pivoted<EN, EM>(p, ls, dw, dc, v, 1, pn);
+#endif
         out(p, B, v, q3);
       }
     }
@@ -1709,7 +1942,11 @@ struct ObcaSolver {
         double v[NL], dpx, dpy;
         rhs(p, B, v, dpx, dpy);
         int pn[2];
+#if HTP_BK_SIMD
+        local_pivoted_v<EN, EM, 1>(p, ls, dw, dc, v, pn);
+#else
         local_pivoted<EN, EM>(p, ls, dw, dc, v, 1, pn);
+#endif
         out(p, B, v, dpx, dpy);
       }
     }

@@ -103,7 +103,7 @@ def run_ulp(name, k, t):
     g = np.load(os.path.join(ROOT, "tests", "golden", "obca_full", f"{name}.npz"))
     inst = load_instance(g)
     tr = np.array(inst["init_traj"], dtype=np.float64)
-    row, col = (k // 2, (k % 2)) if k < 4 else (1 + k, 0)
+    row, col = (k // 2, (k % 2)) if k < 4 else ((1 + k, 0) if k < 8 else (k - 4, 1))
     tr[row, col] = np.nextafter(tr[row, col], np.inf)
     inst = dict(inst, init_traj=tr)
     nlp = ObcaNLP(inst)

@@ -70,7 +70,9 @@ FAILURE_CLASS_ONLY = {
     # the oracle's loop-order variant: 7 after 669 / 24 (witness/E6.npz)
     "E6": "3 vs 7",
     # oracle: Infeasible_Problem_Detected (7) after 1418 iterations / 32 phases; device: the 3000-iteration limit
-    # (2) after 55 phases, with either libm (profiles/r04p_fixture_variants_E12.txt; the round-3 kernel ended 7)
+    # (2) after 55 phases.  The oracle with glibc's transcendental functions (the ones CasADi's SX VM calls) ends 7
+    # after 797 / 18 phases at a point 30.5 m away (witness/E54_libm.npz); the serial host build ends 7 after 868
+    # iterations, and 2, 2, 7, 7, 7 on the instance with one input double moved by one ulp.
     "E54": "7 vs 2",
 }
 # Fixtures the oracle does not solve but the device does: the iterates separate at rounding level inside a
@@ -82,15 +84,17 @@ DIVERGENT_AFTER_RESTORATION = {
     # Solve_Succeeded after 812 / 38 (witness/D347.npz); device: Solve_Succeeded
     "D347": "7 vs 0",
 }
-# Fixtures whose outcome turns on the last bits of the solver's transcendental functions: the device build with
-# the platform libm (ocml) converges like the oracle, the device build with the deterministic libm of
-# csrc/htp_fastm.h (the product: reproducible on the host) and the serial host build (glibc) both stop at the
-# iteration limit (profiles/r04p_fixture_variants_E12.txt, r04_screen_E16.json).  The device must reproduce its
-# host emulation bit for bit (tests/golden/emulation/E12.npz).
+# Fixtures whose outcome the reference algorithm itself does not determine at rounding level: the ORACLE run on the
+# fixture's instance with one input double moved by one ulp (np.nextafter; tests/golden/make_witness.py NAME:ulpK)
+# ends with a different status.  The device must reproduce its host emulation bit for bit
+# (tests/golden/emulation/<name>.npz) and the witness must show the oracle's own status change.
 ROUNDING_DECIDED = {
     # oracle: Solve_Succeeded after 229 iterations / 1 restoration phase; device: Maximum_Iterations_Exceeded
-    # after 3000 / 82; device with ocml: Solve_Succeeded after 218 / 1
-    "E12": "0 vs 2",
+    # after 3000 / 82.  Oracle with init_traj[1, 1] + 1 ulp: Infeasible_Problem_Detected after 826 / 8
+    # (witness/E12_ulp3.npz); with init_traj[2, 0] + 1 ulp: Solve_Succeeded after 2625 / 85 at a point 24.6 m away
+    # (E12_ulp6.npz).  Six further oracle runs (numpy / glibc libm, loop-order elimination, other 1-ulp moves)
+    # converge in 223-316 iterations; the serial host build converges (485 / 2) and fails one of five 1-ulp moves.
+    "E12": ("0 vs 2", "E12_ulp3"),
 }
 # Every divergence above carries two witnesses: the oracle's two elimination orders already disagree on it
 # (tests/golden/witness, make_witness.py), and the device run is reproduced bit for bit by the host emulation
@@ -131,6 +135,8 @@ def test_full_config_parity_vs_oracle_fixtures(ctx, cfg, pid, path):
     res = ctx.solve(_native.PackedBatch([inst]))
     st = int(g["status"])
     if f"{cfg}{pid}" in ROUNDING_DECIDED:
+        w = np.load(os.path.join(WITNESS, ROUNDING_DECIDED[f"{cfg}{pid}"][1] + ".npz"))
+        assert int(w["status_a"]) == st and int(w["status_b"]) != int(w["status_a"])   # the oracle's own split
         e = np.load(os.path.join(EMULATION, f"{cfg}{pid}.npz"))
         assert int(res.status[0]) == int(e["status"]) and int(res.iterations[0]) == int(e["iters"])
         assert np.array_equal(res.x[0].view(np.int64), e["x"].view(np.int64))

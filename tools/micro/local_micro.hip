@@ -25,6 +25,8 @@ __global__ __launch_bounds__(64, 1) void init_ws(const Shape* shp, double* ws_al
   for (int r = threadIdx.x; r < D.md; r += 64) {
     ws[L.s + r] = 0.5 + 0.01 * (r % 5); ws[L.dL + r] = 0.0; ws[L.dU + r] = 2.0; ws[L.vL + r] = 1.0; ws[L.vU + r] = 0.5;
     ws[L.scI + r] = 1.0; ws[L.yd + r] = 0.2; ws[L.rs + r] = 0.01; ws[L.rd + r] = -0.02;
+    // ~1 block in 9: a negative multiplier of ||A' lam||^2 <= 1 makes the lam block indefinite (pivoted path)
+    if ((r & 1) == 0 && ((r / 2) % 9) == 4) ws[L.yd + r] = -50.0;
   }
   for (int r = threadIdx.x; r < D.mc; r += 64) { ws[L.scE + r] = 1.0; ws[L.yc + r] = 0.3 * ((r % 5) - 2); ws[L.rc + r] = 0.01; }
 }
@@ -43,6 +45,7 @@ __global__ __launch_bounds__(64, 1) void micro(const Shape* shp, const double* p
   in.par = prob + 3 * TEo + 3 * TEb;
   ObcaSolver<DevWave, 4, 4, 0> S(c, sh->D, sh->L, sh->o, in, ws);
   long long t[4] = {0, 0, 0, 0};
+  int npiv_tot = 0;
   int nneg = 0;
   using gd = DevWave::gd;
   for (int r = 0; r < reps; ++r) {
@@ -64,6 +67,12 @@ __global__ __launch_bounds__(64, 1) void micro(const Shape* shp, const double* p
     nneg += c.isum(neg);
   }
   if (threadIdx.x == 0) { for (int k = 0; k < 3; ++k) cyc[3 * blockIdx.x + k] = t[k]; negs[blockIdx.x] = nneg; }
+#ifdef HTP_LPROF
+  if (threadIdx.x == 0 && blockIdx.x == 0)
+    printf("[lprof wave 0] factor sweep: pass1 %lld cyc (%lld trips), pass2 %lld cyc (%lld trips, %lld pivoted blocks), "
+           "scan %lld cyc per sweep\n", S.lprof[0] / S.lprof[6], S.lprof[2] / S.lprof[6], S.lprof[1] / S.lprof[6],
+           S.lprof[3] / S.lprof[6], S.lprof[5] / S.lprof[6], S.lprof[4] / S.lprof[6]);
+#endif
 }
 
 int main(int argc, char** argv) {
