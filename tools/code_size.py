@@ -59,6 +59,7 @@ def main():
             cur = m.group(1)
         fn_at[i] = cur
     mix, incl, loc = collections.Counter(), collections.Counter(), None
+    scr_fn, scr_line = collections.Counter(), collections.Counter()   # scratch instructions by function / line
     for line in open(s):
         if line.startswith("\t.loc"):
             loc = line
@@ -74,18 +75,29 @@ def main():
         mix[kind] += 1
         if loc and ";" in loc:
             seen = set()
-            for f, ln in re.findall(r"([\w./-]+\.(?:h|hip)):(\d+):\d+", loc.split(";", 1)[1]):
+            chain = re.findall(r"([\w./-]+\.(?:h|hip)):(\d+):\d+", loc.split(";", 1)[1])
+            if kind == "scratch" and chain:
+                scr_line[f"{os.path.basename(chain[0][0])}:{chain[0][1]}"] += 1
+            for f, ln in chain:
                 if f.endswith("obca_core.h"):
                     fn = fn_at.get(int(ln), "?")
                     if fn not in seen:
                         seen.add(fn)
                         incl[fn] += 1
+                        if kind == "scratch":
+                            scr_fn[fn] += 1
     print(f"instructions {sum(mix.values())} {dict(mix)}")
     print("resources", {k: res[k] for k in res if k in ("VGPRs", "AGPRs", "ScratchSize [bytes/lane]",
                                                          "VGPRs Spill", "SGPRs Spill", "LDS Size [bytes/block]")})
     print("inclusive instructions per obca_core.h function (all inlined copies):")
     for fn, v in incl.most_common(30):
         print(f"  {fn:28s} {v}")
+    print("scratch instructions per obca_core.h function (inclusive):")
+    for fn, v in scr_fn.most_common(25):
+        print(f"  {fn:28s} {v}")
+    print("scratch instructions per source line (innermost):")
+    for ln, v in scr_line.most_common(40):
+        print(f"  {ln:28s} {v}")
 
 
 if __name__ == "__main__":

@@ -11,6 +11,7 @@
 #     pytest:FILE[,FILE...]   only these GPU test files (tests/FILE)
 #     pytestk:FILE[,...]      the same, every test (no -x, output shown) and the script goes on after test failures
 #     benchC / benchE / benchD20   config C at 6 steps, config E, config D at 20 steps
+#     ychain16k  notebook planner chain e2e at 16 384 scenes (cached draws), then its rocprofv3 kernel stats
 #     pmcC / pmcE    PMC passes for configs C / E only
 #     stall    the three SQ stall passes (tools/gpu_stall.sh) on config D
 #     diag     I-cache / TLB / L2 / L1 passes (tools/gpu_diag.sh) on config D
@@ -64,6 +65,10 @@ for S in "$@"; do
              run benchB 200 python -u bench.py --config B --steps 6 --no-cpu-baseline ;;
     e2eC) run e2eC 600 python -u bench.py --e2e --config C --steps 3 --warmup 1 ;;
     ychain) run ychain 600 python -u bench.py --e2e --planner ypark_hastar --steps 3 --warmup 1 ;;
+    ychain16k) run ychaingen 300 python -u bench.py --e2e --planner ypark_hastar --batch 16384 --gen-only --cache /tmp/htp_ycache
+           run ychain16k 600 python -u bench.py --e2e --planner ypark_hastar --batch 16384 --steps 2 --warmup 1 --cache /tmp/htp_ycache
+           run ychainkt 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_ychainkt -o ykt -- \
+               python3 -u bench.py --e2e --planner ypark_hastar --batch 16384 --steps 1 --warmup 0 --cache /tmp/htp_ycache ;;
     benchC) run benchC 600 python -u bench.py --config C --steps 6 --no-cpu-baseline ;;
     benchE) run benchE 900 python -u bench.py --config E --steps 1 --warmup 0 --no-cpu-baseline ;;
     benchE512) run benchE512 900 python -u bench.py --config E --steps 1 --warmup 0 --no-cpu-baseline --waves 512 ;;
