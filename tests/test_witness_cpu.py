@@ -16,7 +16,7 @@ STATE_TOL = 1e-4
 
 # fixture -> the witness files that must show a divergence
 REQUIRED = {"D347": ["D347"], "E6": ["E6"], "E84": ["E84"], "P19": ["P19"], "E12": ["E12_ulp3", "E12_ulp6"],
-            "E54": ["E54_libm"]}
+            "E54": ["E54_libm", "E54_ulp1"]}
 
 
 def _diverges(w):
@@ -37,3 +37,10 @@ def test_e12_status_split_and_record():
     assert int(w["status_a"]) == 0 and int(w["status_b"]) == 7
     agree = [f for f in os.listdir(W) if f.startswith("E12_") and not _diverges(np.load(os.path.join(W, f)))]
     assert len(agree) >= 5, agree
+
+
+def test_e54_status_split():
+    """E54: the fixture (Infeasible_Problem_Detected, 1418 iterations / 32 phases) against the same instance with
+    init_traj[0, 1] one ulp up: the oracle converges (Solve_Succeeded after 652 / 2 phases)."""
+    w = np.load(os.path.join(W, "E54_ulp1.npz"))
+    assert int(w["status_a"]) == 7 and int(w["status_b"]) == 0
