@@ -15,6 +15,7 @@
 // sweeps is wave-uniform.
 #pragma once
 #include <cmath>
+#include <type_traits>
 
 #include "htp_common.h"
 #include "htp_fastm.h"
@@ -405,12 +406,44 @@ HTP_HD inline void bk_solve_packed(T* K, const int* ip, int n, double* v) {
 // bk_factor_packed / bk_solve_packed above in the same order, so factors, inertia and solutions are bit-identical.
 template <int S, class T>
 HTP_HD HTP_FI inline T& pkx(T* K, int r, int c) { return K[S * (r >= c ? r * (r + 1) / 2 + c : c * (c + 1) / 2 + r)]; }
+// The empty asm hands each element to the select chain as a register value: without it InstCombine turns the
+// chain of selects between loads v[j] into one load from a select between their addresses, a run-time index that
+// keeps the whole array (pivot vector, right-hand sides) in scratch memory instead of registers.
+#ifndef HTP_J8
+#define HTP_J8 1
+#endif
+#ifndef HTP_SEL_OPAQUE
+#define HTP_SEL_OPAQUE 0
+#endif
+#ifndef HTP_BK_BATCH
+#define HTP_BK_BATCH 1
+#endif
+template <class V>
+HTP_HD HTP_FI inline V sel_opaque(V x) {
+#if defined(__HIP_DEVICE_COMPILE__) && HTP_SEL_OPAQUE
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+#ifndef HTP_SEL_MASK
+#define HTP_SEL_MASK 0
+#endif
 template <int n, class V>
 HTP_HD HTP_FI inline V sel_get(const V* v, int k) {
-  V r = v[0];
+#if HTP_SEL_MASK
+  // v[k] as an OR of masked bit patterns (exactly one mask is all ones): no select of loads for InstCombine to
+  // fold into a run-time address
+  using U = typename std::conditional<sizeof(V) == 8, unsigned long long, unsigned int>::type;
+  U r = 0;
 #pragma unroll
-  for (int j = 1; j < n; ++j) r = (k == j) ? v[j] : r;
+  for (int j = 0; j < n; ++j) r |= __builtin_bit_cast(U, v[j]) & (U)(-(long long)(k == j));
+  return __builtin_bit_cast(V, r);
+#else
+  V r = sel_opaque(v[0]);
+#pragma unroll
+  for (int j = 1; j < n; ++j) r = (k == j) ? sel_opaque(v[j]) : r;
   return r;
+#endif
 }
 template <int n>
 HTP_HD HTP_FI inline void sel_set(double* v, int k, double x) {
@@ -586,6 +619,216 @@ HTP_HD HTP_FI inline void bk_solve_simd(T* K, const int* ip, double* v) {
   }
 }
 
+// bk_factor_simd / bk_solve_simd with every step's loads issued together (HTP_BK_BATCH, the default).  In the
+// forms above each element's read-modify-write sits under its own per-lane predicate and reads a run-time-indexed
+// element (column k) that may alias the previous write, so on the device every one of the ~1 500 LDS accesses of a
+// factorization waited a full LDS round trip.  Here each step first loads what it reads (column k, the rows to
+// interchange), then updates constant-offset elements with select-stores; the column values are the ones the
+// original loop reads (an update never writes column k, and the 2 x 2 branch's descending row order already
+// read the original columns), every element gets the same expression in the same order: bit-identical.
+template <int n, int S, class T>
+HTP_HD HTP_FI inline void bk_factor_batch(T* K, int* ip, int& neg, int& zero) {
+  const double alpha = 0.6403882032022076;
+  neg = 0;
+  zero = 0;
+#pragma unroll
+  for (int j = 0; j < n; ++j) ip[j] = 0;
+  int k = 0;
+#pragma unroll 1
+  for (int step = 0; step < n; ++step) {
+    const bool act = k < n;
+    const int kc = act ? k : 0;
+    int kstep = 1, kp = kc;
+    double cs[n];                                  // K(r, kc) for r > kc (r <= kc: in-bounds, unused)
+#pragma unroll
+    for (int r = 0; r < n; ++r) cs[r] = K[S * (r * (r + 1) / 2 + kc)];
+    const double absakk = fabs((double)K[S * (kc * (kc + 1) / 2 + kc)]);
+    int imax = kc;
+    double colmax = 0.0;
+#pragma unroll
+    for (int r = 1; r < n; ++r) {
+      const double v = fabs(cs[r]);
+      const bool t = r > kc && v > colmax;
+      colmax = t ? v : colmax;
+      imax = t ? r : imax;
+    }
+    if (act && !(absakk >= alpha * colmax) && !(absakk == 0.0 && colmax == 0.0)) {
+      double rw[n];
+#pragma unroll
+      for (int j = 0; j < n; ++j) rw[j] = fabs((double)pkx<S>(K, imax, j));
+      const double dmax = fabs((double)K[S * (imax * (imax + 1) / 2 + imax)]);
+      double rowmax = 0.0;
+#pragma unroll
+      for (int j = 0; j < n; ++j) rowmax = (j >= kc && j != imax && rw[j] > rowmax) ? rw[j] : rowmax;
+      if (absakk >= alpha * colmax * (colmax / rowmax)) kp = kc;
+      else if (dmax >= alpha * rowmax) kp = imax;
+      else { kp = imax; kstep = 2; }
+    }
+    const int kk = kc + kstep - 1;
+    if (act && kp != kk) {                         // the interchanged elements are distinct: load all, then store
+      double a[n], b[n];
+#pragma unroll
+      for (int j = 0; j < n; ++j) { a[j] = pkx<S>(K, kk, j); b[j] = pkx<S>(K, kp, j); }
+      const double dk = K[S * (kk * (kk + 1) / 2 + kk)], dp = K[S * (kp * (kp + 1) / 2 + kp)];
+#pragma unroll
+      for (int j = 0; j < n; ++j)
+        if (j >= kc && j != kk && j != kp) { pkx<S>(K, kk, j) = b[j]; pkx<S>(K, kp, j) = a[j]; }
+      K[S * (kk * (kk + 1) / 2 + kk)] = dp;
+      K[S * (kp * (kp + 1) / 2 + kp)] = dk;
+    }
+    if (act && kstep == 1) {
+      double c[n];
+#pragma unroll
+      for (int r = 0; r < n; ++r) c[r] = K[S * (r * (r + 1) / 2 + kc)];
+      double d = K[S * (kc * (kc + 1) / 2 + kc)];
+      if (d == 0.0) { zero = 1; d = 1.0; K[S * (kc * (kc + 1) / 2 + kc)] = 1.0; }
+      if (d < 0.0) ++neg;
+      const double id = 1.0 / d;
+      double lr[n];
+#pragma unroll
+      for (int r = 0; r < n; ++r) lr[r] = (r > kc) ? c[r] * id : 0.0;
+#pragma unroll
+      for (int r = 1; r < n; ++r)
+#pragma unroll
+        for (int q = 1; q <= r; ++q) {
+          T& e = K[S * (r * (r + 1) / 2 + q)];
+          const double kv = e;
+          const double nv = kv - lr[r] * c[q];
+          e = (q > kc) ? nv : kv;
+        }
+#pragma unroll
+      for (int r = 1; r < n; ++r)
+        if (r > kc) K[S * (r * (r + 1) / 2 + kc)] = c[r] * id;
+#pragma unroll
+      for (int j = 0; j < n; ++j) ip[j] = (j == kc) ? kp : ip[j];
+    } else if (act) {
+      double ca[n], cb[n];
+#pragma unroll
+      for (int r = 0; r < n; ++r) {
+        ca[r] = K[S * (r * (r + 1) / 2 + kc)];
+        cb[r] = K[S * (r * (r + 1) / 2 + (kc + 1 < n ? kc + 1 : kc))];
+      }
+      const double d11 = K[S * (kc * (kc + 1) / 2 + kc)], d21 = K[S * ((kc + 1) * (kc + 2) / 2 + kc)];
+      const double d22 = K[S * ((kc + 1) * (kc + 2) / 2 + kc + 1)];
+      const double det = d11 * d22 - d21 * d21;
+      if (det < 0.0) neg += 1;
+      else if (det > 0.0) neg += (d11 + d22 < 0.0) ? 2 : 0;
+      else zero = 1;
+      const double i11 = d22 / det, i22 = d11 / det, i21 = -d21 / det;
+      double l1[n], l2[n];
+#pragma unroll
+      for (int r = 0; r < n; ++r) {
+        const double a1 = ca[r], a2 = cb[r];
+        l1[r] = a1 * i11 + a2 * i21;
+        l2[r] = a1 * i21 + a2 * i22;
+      }
+#pragma unroll
+      for (int r = 2; r < n; ++r)
+#pragma unroll
+        for (int q = 2; q <= r; ++q) {
+          T& e = K[S * (r * (r + 1) / 2 + q)];
+          const double kv = e;
+          const double nv = kv - (l1[r] * ca[q] + l2[r] * cb[q]);
+          e = (q >= kc + 2) ? nv : kv;
+        }
+#pragma unroll
+      for (int r = 2; r < n; ++r)
+        if (r >= kc + 2) {
+          K[S * (r * (r + 1) / 2 + kc)] = l1[r];
+          K[S * (r * (r + 1) / 2 + kc + 1)] = l2[r];
+        }
+#pragma unroll
+      for (int j = 0; j < n; ++j) ip[j] = (j == kc || j == kc + 1) ? -(kp + 1) : ip[j];
+    }
+    k += act ? kstep : 0;
+  }
+}
+
+template <int n, int S, class T>
+HTP_HD HTP_FI inline void bk_solve_batch(const T* K, const int* ip, double* v) {
+  int k = 0;
+#pragma unroll 1
+  for (int step = 0; step < n; ++step) {          // forward: P, L, D
+    const bool act = k < n;
+    const int kc = act ? k : 0;
+    const int ipk = sel_get<n>(ip, kc);
+    const int kc1 = kc + 1 < n ? kc + 1 : kc;
+    double ca[n], cb[n];
+#pragma unroll
+    for (int r = 0; r < n; ++r) { ca[r] = K[S * (r * (r + 1) / 2 + kc)]; cb[r] = K[S * (r * (r + 1) / 2 + kc1)]; }
+    const double d11 = K[S * (kc * (kc + 1) / 2 + kc)], d21 = K[S * (kc1 * (kc1 + 1) / 2 + kc)];
+    const double d22 = K[S * (kc1 * (kc1 + 1) / 2 + kc1)];
+    if (act && ipk >= 0) {
+      const int kp = ipk;
+      if (kp != kc) { const double a = sel_get<n>(v, kc), b = sel_get<n>(v, kp); sel_set<n>(v, kc, b); sel_set<n>(v, kp, a); }
+      const double vk = sel_get<n>(v, kc);
+#pragma unroll
+      for (int r = 1; r < n; ++r) {
+        const double nv = v[r] - ca[r] * vk;
+        v[r] = (r > kc) ? nv : v[r];
+      }
+#pragma unroll
+      for (int j = 0; j < n; ++j) v[j] = (j == kc) ? v[j] / d11 : v[j];
+      k += 1;
+    } else if (act) {
+      const int kp = -ipk - 1;
+      if (kp != kc + 1) {
+        const double a = sel_get<n>(v, kc + 1), b = sel_get<n>(v, kp);
+        sel_set<n>(v, kc + 1, b);
+        sel_set<n>(v, kp, a);
+      }
+      const double vk = sel_get<n>(v, kc), vk1 = sel_get<n>(v, kc + 1);
+#pragma unroll
+      for (int r = 2; r < n; ++r) {
+        const double nv = v[r] - (ca[r] * vk + cb[r] * vk1);
+        v[r] = (r > kc + 1) ? nv : v[r];
+      }
+      const double det = d11 * d22 - d21 * d21;
+      const double b1 = vk, b2 = vk1;
+      sel_set<n>(v, kc, (d22 * b1 - d21 * b2) / det);
+      sel_set<n>(v, kc + 1, (-d21 * b1 + d11 * b2) / det);
+      k += 2;
+    }
+  }
+  k = n - 1;
+#pragma unroll 1
+  for (int step = 0; step < n; ++step) {          // backward: L', P'
+    const bool act = k >= 0;
+    const int kc = act ? k : 0;
+    const int ipk = sel_get<n>(ip, kc);
+    const int km = kc >= 1 ? kc - 1 : 0;
+    double ca[n], cm[n];
+#pragma unroll
+    for (int r = 0; r < n; ++r) { ca[r] = K[S * (r * (r + 1) / 2 + kc)]; cm[r] = K[S * (r * (r + 1) / 2 + km)]; }
+    if (act && ipk >= 0) {
+      double t = sel_get<n>(v, kc);
+#pragma unroll
+      for (int r = 1; r < n; ++r) {
+        const double nt = t - ca[r] * v[r];
+        t = (r > kc) ? nt : t;
+      }
+      sel_set<n>(v, kc, t);
+      const int kp = ipk;
+      if (kp != kc) { const double a = sel_get<n>(v, kc), b = sel_get<n>(v, kp); sel_set<n>(v, kc, b); sel_set<n>(v, kp, a); }
+      k -= 1;
+    } else if (act) {
+      double t = sel_get<n>(v, kc), t1 = sel_get<n>(v, km);
+#pragma unroll
+      for (int r = 1; r < n; ++r) {
+        const double nt = t - ca[r] * v[r];
+        const double nt1 = t1 - cm[r] * v[r];
+        t = (r > kc) ? nt : t;
+        t1 = (r > kc) ? nt1 : t1;
+      }
+      sel_set<n>(v, kc, t);
+      sel_set<n>(v, km, t1);
+      const int kp = -ipk - 1;
+      if (kp != kc) { const double a = sel_get<n>(v, kc), b = sel_get<n>(v, kp); sel_set<n>(v, kc, b); sel_set<n>(v, kp, a); }
+      k -= 2;
+    }
+  }
+}
+
 // LDS ring of the matrix-core Riccati passes (ObcaSolver::ring_fill): RING_SB + 1 stage records of
 // RS_L doubles (LD slot prefix [0, SOFF + NS), V_i, X_i) after the per-wave scratch and filter.
 #ifndef HTP_RING_SB
@@ -664,10 +907,22 @@ struct ObcaSolver {
 #define HTP_KPROF(k, t) do { } while (0)
 #endif
 #ifdef HTP_LPROF  // experiments: the local factor sweep -- pass 1 / pass 2 / inertia-scan cycles, trip counts (Result::cyc)
-  long long lprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // HTP_LPROF=2: pass 2 split instead of pass 1 and the trip counts: build_local (slot 0), Bunch-Kaufman factor
+  // (slot 2), the right-hand-side solves with their fills and outputs (slot 3)
+  mutable long long lprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  mutable long long lp2_t = 0;
 #define HTP_LP(k, v) do { lprof[k] += (v); } while (0)
+#if HTP_LPROF == 2
+#define HTP_LP1(k, v) do { } while (0)
+#define HTP_LP2(k, v) do { lprof[k] += (v); } while (0)
+#else
+#define HTP_LP1(k, v) do { lprof[k] += (v); } while (0)
+#define HTP_LP2(k, v) do { } while (0)
+#endif
 #else
 #define HTP_LP(k, v) do { } while (0)
+#define HTP_LP1(k, v) do { } while (0)
+#define HTP_LP2(k, v) do { } while (0)
 #endif
 #ifdef HTP_PROF_ON  // experiments: sub-step cycle counters of the stage chain (tools/build_variants.py)
   long long pcyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -760,6 +1015,27 @@ struct ObcaSolver {
   HTP_HD HTP_FI void dynJ(const double* w, double* J) const {
     if (D.topt) dyn_J_rk2(w, par(P_DT), par(P_WHEELBASE), J);
     else dyn_J_euler(w, par(P_DT), par(P_WHEELBASE), J);
+  }
+  // The same Jacobian at a fixed row stride of 8 (J8[k * 8 + j], j < D.nw; the rest 0): constant offsets for any
+  // nw, so the array stays in registers (a run-time stride D.nw sends it to scratch memory).
+  HTP_HD HTP_FI void dynJ8(const double* w, double* J8) const {
+#if !HTP_J8
+    double J[40];
+    dynJ(w, J);
+    for (int k = 0; k < NS; ++k)
+      for (int j = 0; j < 8; ++j) J8[k * 8 + j] = j < D.nw ? J[k * D.nw + j] : 0.0;
+    return;
+#endif
+    if (D.topt) {
+      dyn_J_rk2(w, par(P_DT), par(P_WHEELBASE), J8);
+    } else {
+      double J7[NS * 7];
+      dyn_J_euler(w, par(P_DT), par(P_WHEELBASE), J7);
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) J8[k * 8 + j] = j < 7 ? J7[k * 7 + j] : 0.0;
+    }
   }
   HTP_HD HTP_FI void dynH(const double* w, const double* y, double* H) const {
     if (D.topt) dyn_H_rk2(w, par(P_DT), par(P_WHEELBASE), y, H);
@@ -1107,10 +1383,13 @@ struct ObcaSolver {
       } else {
         double w[8], J[40], yy[5];
         stage_w(x, i, w);
-        dynJ(w, J);
+        dynJ8(w, J);
         for (int k = 0; k < NS; ++k) yy[k] = scE[D.eDyn + NS * i + k] * yc[D.eDyn + NS * i + k];
+#pragma unroll
         for (int k = 0; k < NS; ++k)
-          for (int j = 0; j < D.nw; ++j) gw[j] -= J[k * D.nw + j] * yy[k];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < D.nw) gw[j] -= J[k * 8 + j] * yy[k];
         for (int k = 0; k < NS; ++k) gx[k] += gw[k];
       }
       for (int q = 0; q < MK; ++q) {
@@ -1203,10 +1482,13 @@ struct ObcaSolver {
       if (i < N - 1) {
         double w[8], J[40];
         stage_w(x, i, w);
-        dynJ(w, J);
+        dynJ8(w, J);
+#pragma unroll
         for (int k = 0; k < NS; ++k) {
           double rm = 1.0;  // +1 at x_{i+1,k}
-          for (int j = 0; j < D.nw; ++j) rm = dmax(rm, dabs(J[k * D.nw + j]));
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < D.nw) rm = dmax(rm, dabs(J[k * 8 + j]));
           scE[D.eDyn + NS * i + k] = scl(rm);
         }
       } else {
@@ -1530,30 +1812,62 @@ struct ObcaSolver {
     for (int k = 0; k < nrhs; ++k) bk_solve_packed(B.K, ip, NL, V + k * NL);
   }
 
-  // local_pivoted as SIMD-convergent code (bk_factor_simd / bk_solve_simd), inlined so that the NRHS right-hand
-  // sides V[c * NL + r] stay in registers; on the device the block goes to this lane's interleaved slice of the
-  // LDS ring region (element e at lds[RING_OFF + 64 e + lane]).  Bit-identical to local_pivoted.
-  template <int EN, int EM, int NRHS>
-  HTP_HD HTP_FI void local_pivoted_v(int p, bool ls, double dw, double dc, double* V, int* inertia) const {
+  // local_pivoted as SIMD-convergent code (bk_factor_simd / bk_solve_simd), inlined; on the device the block goes
+  // to this lane's interleaved slice of the LDS ring region (element e at lds[RING_OFF + 64 e + lane]).  The NRHS
+  // right-hand sides are solved one at a time: col(k, v, false) fills v with column k, col(k, v, true) consumes
+  // its solution, so only one column is live in registers (all four at once pushed the kernel into spills).
+  // Bit-identical to local_pivoted.  B: the block as build_local returned it (not factored).
+  template <int EN, int EM, int NRHS, class Col>
+  HTP_HD HTP_FI void local_pivoted_v(const LocalBlock<EN, EM>& B, Col&& col, int* inertia) const {
     constexpr int NL = LocalBlock<EN, EM>::NL;
     constexpr int NPK = LocalBlock<EN, EM>::NPK;
-    LocalBlock<EN, EM> B;
-    build_local<EN, EM>(B, p, ls, dw, dc);
     int ip[NL];
 #if defined(__HIPCC__) || defined(HTP_EMU_WAVE)
     if constexpr (Ctx::kMfma && HTP_PIV_LDS && NPK <= PIV_LDS_PER_LANE) {
       ld* K = c.lds + RING_OFF + c.lane;
 #pragma unroll
       for (int q = 0; q < NPK; ++q) K[64 * q] = B.K[q];
+#if HTP_BK_BATCH
+      bk_factor_batch<NL, 64>(K, ip, inertia[0], inertia[1]);
+#else
       bk_factor_simd<NL, 64>(K, ip, inertia[0], inertia[1]);
+#endif
+#if defined(HTP_LPROF) && HTP_LPROF == 2
+      lp2_t = c.clock();
+#endif
 #pragma unroll
-      for (int k = 0; k < NRHS; ++k) bk_solve_simd<NL, 64>(K, ip, V + k * NL);
+      for (int k = 0; k < NRHS; ++k) {
+        double v[NL];
+        col(k, v, false);
+#if HTP_BK_BATCH
+        bk_solve_batch<NL, 64>(K, ip, v);
+#else
+        bk_solve_simd<NL, 64>(K, ip, v);
+#endif
+        col(k, v, true);
+      }
       return;
     }
 #endif
-    bk_factor_simd<NL, 1>(B.K, ip, inertia[0], inertia[1]);
+    double K[NPK];
 #pragma unroll
-    for (int k = 0; k < NRHS; ++k) bk_solve_simd<NL, 1>(B.K, ip, V + k * NL);
+    for (int q = 0; q < NPK; ++q) K[q] = B.K[q];
+#if HTP_BK_BATCH
+    bk_factor_batch<NL, 1>(K, ip, inertia[0], inertia[1]);
+#else
+    bk_factor_simd<NL, 1>(K, ip, inertia[0], inertia[1]);
+#endif
+#pragma unroll
+    for (int k = 0; k < NRHS; ++k) {
+      double v[NL];
+      col(k, v, false);
+#if HTP_BK_BATCH
+      bk_solve_batch<NL, 1>(K, ip, v);
+#else
+      bk_solve_simd<NL, 1>(K, ip, v);
+#endif
+      col(k, v, true);
+    }
   }
 
   // LocalStore record of block p (HTP_STORE_LOCAL): written by the factor sweep, read by the solve sweeps
@@ -1649,7 +1963,8 @@ struct ObcaSolver {
     if (!B.piv) { nb = B.neg; zb = B.zero ? 1 : 0; return; }
     int pn[2];
 #if HTP_BK_SIMD
-    local_pivoted_v<EN, EM, 0>(p, ls, dw, dc, nullptr, pn);
+    build_local<EN, EM>(B, p, ls, dw, dc);   // B.factor() overwrote the block
+    local_pivoted_v<EN, EM, 0>(B, [](int, double*, bool) {}, pn);
 #else
     local_pivoted<EN, EM>(p, ls, dw, dc, nullptr, 0, pn);
 #endif
@@ -1691,7 +2006,7 @@ struct ObcaSolver {
     for (int b0 = 0; b0 < D.P; b0 += c.width) {
       const int p = b0 + c.lane;
       bool piv = false;
-      HTP_LP(2, 1);
+      HTP_LP1(2, 1);
       if (p < D.P) {
         LocalBlock<EN, EM> B;
         build_local<EN, EM>(B, p, ls, dw, dc);
@@ -1743,39 +2058,69 @@ struct ObcaSolver {
     c.sync();
 #ifdef HTP_LPROF
     const long long lt1 = c.clock();
-    HTP_LP(0, lt1 - lt0);
+    HTP_LP1(0, lt1 - lt0);
     HTP_LP(4, (long long)c.maxv((double)lscan));
     HTP_LP(5, npiv);
     HTP_LP(6, 1);
 #endif
     for (int b0 = 0; b0 < npiv; b0 += c.width) {
       const int q = b0 + c.lane;
-      HTP_LP(3, 1);
+      HTP_LP1(3, 1);
       if (q < npiv) {
         const int p = (int)PL[q];
         LocalBlock<EN, EM> B;
+#if defined(HTP_LPROF) && HTP_LPROF == 2
+        const long long q0 = c.clock();
+#endif
         build_local<EN, EM>(B, p, ls, dw, dc);
+#if defined(HTP_LPROF) && HTP_LPROF == 2
+        const long long q1 = c.clock();
+        HTP_LP2(0, q1 - q0);
+#endif
+        int pn[2];
+        double S[6];
+#if HTP_BK_SIMD
+        double q3 = 0.0;
+        auto colf = [&](int col, double* v, bool done) {
+          if (col < 3) {
+            if (!done) {
+              for (int r = 0; r < NL; ++r) v[r] = B.B[r][col];
+            } else {
+              for (int row = 0; row <= col; ++row) {  // S(:,col) = B' K^-1 B(:,col)
+                double acc = 0.0;
+                for (int r = 0; r < NL; ++r) acc += B.B[r][row] * v[r];
+                S[sidx(row, col)] = acc;
+              }
+            }
+          } else if (!done) {
+            local_rhs_vec<EN, EM>(p, B, A(L.xt), A(L.rs), A(L.rc), A(L.rd), v, q3);
+          } else {
+            local_rhs_out<EN, EM>(p, B, v, q3, A(L.pairR));
+          }
+        };
+        if (fuse_rhs) local_pivoted_v<EN, EM, 4>(B, colf, pn);
+        else local_pivoted_v<EN, EM, 3>(B, colf, pn);
+#if defined(HTP_LPROF) && HTP_LPROF == 2
+        const long long q2 = c.clock();
+        HTP_LP2(2, lp2_t - q1);
+        HTP_LP2(3, q2 - lp2_t);
+#endif
+#else
         double Vp[4 * NL], q3 = 0.0;
         for (int col = 0; col < 3; ++col)
           for (int r = 0; r < NL; ++r) Vp[col * NL + r] = B.B[r][col];
         if (fuse_rhs) local_rhs_vec<EN, EM>(p, B, A(L.xt), A(L.rs), A(L.rc), A(L.rd), Vp + 3 * NL, q3);
-        int pn[2];
-#if HTP_BK_SIMD
-        if (fuse_rhs) local_pivoted_v<EN, EM, 4>(p, ls, dw, dc, Vp, pn);
-        else local_pivoted_v<EN, EM, 3>(p, ls, dw, dc, Vp, pn);
-#else
         local_pivoted<EN, EM>(p, ls, dw, dc, Vp, fuse_rhs ? 4 : 3, pn);
-#endif
         if (fuse_rhs) local_rhs_out<EN, EM>(p, B, Vp + 3 * NL, q3, A(L.pairR));
-        neg += pn[0];
-        zero |= pn[1];
-        double S[6];
         for (int col = 0; col < 3; ++col)
           for (int row = 0; row <= col; ++row) {  // S(:,col) = B' K^-1 B(:,col)
             double acc = 0.0;
             for (int r = 0; r < NL; ++r) acc += B.B[r][row] * Vp[col * NL + r];
             S[sidx(row, col)] = acc;
           }
+#endif
+        neg += pn[0];
+        zero |= pn[1];
         for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
         if (ic_scan) scan(p, pn[0], pn[1]);
       }
@@ -1839,15 +2184,19 @@ struct ObcaSolver {
         const int p = (int)PL[q];
         LocalBlock<EN, EM> B;
         build_local<EN, EM>(B, p, ls, dw, dc);
-        double v[NL], q3;
-        rhs(p, B, v, q3);
         int pn[2];
 #if HTP_BK_SIMD
-        local_pivoted_v<EN, EM, 1>(p, ls, dw, dc, v, pn);
+        double q3;
+        local_pivoted_v<EN, EM, 1>(B, [&](int, double* v, bool done) {
+          if (!done) rhs(p, B, v, q3);
+          else out(p, B, v, q3);
+        }, pn);
 #else
+        double v[NL], q3;
+        rhs(p, B, v, q3);
         local_pivoted<EN, EM>(p, ls, dw, dc, v, 1, pn);
-#endif
         out(p, B, v, q3);
+#endif
       }
     }
   }
@@ -1939,15 +2288,19 @@ struct ObcaSolver {
         const int p = (int)PL[q];
         LocalBlock<EN, EM> B;
         build_local<EN, EM>(B, p, ls, dw, dc);
-        double v[NL], dpx, dpy;
-        rhs(p, B, v, dpx, dpy);
         int pn[2];
 #if HTP_BK_SIMD
-        local_pivoted_v<EN, EM, 1>(p, ls, dw, dc, v, pn);
+        double dpx, dpy;
+        local_pivoted_v<EN, EM, 1>(B, [&](int, double* v, bool done) {
+          if (!done) rhs(p, B, v, dpx, dpy);
+          else out(p, B, v, dpx, dpy);
+        }, pn);
 #else
+        double v[NL], dpx, dpy;
+        rhs(p, B, v, dpx, dpy);
         local_pivoted<EN, EM>(p, ls, dw, dc, v, 1, pn);
-#endif
         out(p, B, v, dpx, dpy);
+#endif
       }
     }
   }
@@ -2390,13 +2743,17 @@ struct ObcaSolver {
       }
       double w[8], J[40];
       stage_w(x, i, w);
-      dynJ(w, J);
+      dynJ8(w, J);
       gd* Js = A(L.LD) + (int64_t)i * nb * nb + JOFF;  // unscaled J_i (stride 8) for the Riccati records
+#pragma unroll
       for (int k = 0; k < NS; ++k) {
         const double s_ = scE[D.eDyn + NS * i + k];
         if (!compact)
-          for (int j = 0; j < D.nw; ++j) O[k * nb + NS + j] = -s_ * J[k * D.nw + j];
-        for (int j = 0; j < 8; ++j) Js[k * 8 + j] = (j < D.nw) ? J[k * D.nw + j] : 0.0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < D.nw) O[k * nb + NS + j] = -s_ * J[k * 8 + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Js[k * 8 + j] = J[k * 8 + j];
       }
       if (PT && !ls && i < N - 2) {
         const int U0 = NS + 5;

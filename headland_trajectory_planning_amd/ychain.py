@@ -82,8 +82,13 @@ def make_scene(pid, key=20261017):
                 continue                     # the combined planner would drive forward: not this chain's case
         except (ValueError, IndexError):
             pass
-        return dict(pid=pid, seed=seed, rows=np.asarray(rows), env=env, start=np.asarray(start, float),
-                    end=np.asarray(end, float), eps_seed=seed + 7)
+        scene = dict(pid=pid, seed=seed, rows=np.asarray(rows), env=env, start=np.asarray(start, float),
+                     end=np.asarray(end, float), eps_seed=seed + 7)
+        try:   # the notebook's OBCA obstacle builder raises (IndexError) when no boundary polygon flanks the turn
+            obca_obstacles(scene, 6)
+        except (IndexError, ValueError):
+            continue
+        return scene
     raise RuntimeError(f"[ychain] scene {pid}: no row pair needing the Y-park chain in 64 draws")
 
 

@@ -39,7 +39,13 @@ for rnd in range(2):
             if "kp2" in k:   # HTP_KKT_PROF=2: rhs sweep, stage rhs, Riccati backward, forward, ric+scatter, back sweep, n_kkt
                 nm = ["rhs_sweep", "stage_rhs", "ric_bwd", "ric_fwd", "total", "ric+scatter", "back_sweep", "n_kkt"]
                 line += " | kkt solves per iteration %.3f" % (cyc[:, 7].sum() / max(1, r.iterations.sum()))
-            if "lp" in k.split("_")[0] and "prof" not in k:   # HTP_LPROF: local factor sweep
+            if "lq" in k.split("_")[0]:   # HTP_LPROF=2: pass 2 split (build, factor, solves)
+                nm = ["p2_build", "pass2_cyc", "p2_factor", "p2_solves", "total", "scan_cyc", "n_piv", "n_sweeps"]
+                sw = max(1.0, cyc[:, 7].sum())
+                line += " | per sweep: pass2 %.0f cyc = build %.0f + factor %.0f + solves %.0f, %.1f pivoted blocks" % (
+                        cyc[:, 1].sum() / sw, cyc[:, 0].sum() / sw, cyc[:, 2].sum() / sw, cyc[:, 3].sum() / sw,
+                        cyc[:, 6].sum() / sw)
+            elif "lp" in k.split("_")[0] and "prof" not in k:   # HTP_LPROF: local factor sweep
                 nm = ["pass1_cyc", "pass2_cyc", "pass1_trips", "pass2_trips", "total", "scan_cyc", "n_piv", "n_sweeps"]
                 sw = max(1.0, cyc[:, 7].sum())
                 line += " | per sweep: pass1 %.0f cyc (%.2f trips), pass2 %.0f cyc (%.2f trips), scan %.0f cyc, %.1f " \

@@ -70,7 +70,7 @@ for S in "$@"; do
            run ychainkt 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_ychainkt -o ykt -- \
                python3 -u bench.py --e2e --planner ypark_hastar --batch 16384 --steps 1 --warmup 0 --cache /tmp/htp_ycache ;;
     benchC) run benchC 600 python -u bench.py --config C --steps 6 --no-cpu-baseline ;;
-    benchE) run benchE 900 python -u bench.py --config E --steps 1 --warmup 0 --no-cpu-baseline ;;
+    benchE) run benchE 900 python -u bench.py --config E --steps 2 --warmup 0 --no-cpu-baseline ;;
     benchE512) run benchE512 900 python -u bench.py --config E --steps 1 --warmup 0 --no-cpu-baseline --waves 512 ;;
     benchD20) run benchD20 900 python -u bench.py --steps 20 --no-cpu-baseline ;;
     pmcC) bash tools/gpu_pmc.sh ${T}C --config C --batch 4096 || exit 1 ;;
