@@ -153,7 +153,9 @@ struct Footprint {
   // quads the planners lower (tree rows, obstacle squares) some edge normal separates them by a comparable
   // amount, far above rounding -- the full test returns false for it too.
   static constexpr double SAT_EPS = 1e-6;
+  template <int NBC>
   HTP_HD bool sat_hit(const double* bx, const double* by, int p) const {
+    const int nb = NBC ? NBC : this->nb;
     const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
     const double* V = g.vert + 2 * o;
     {
@@ -204,7 +206,9 @@ struct Footprint {
     return true;
   }
 
+  template <int NBC>
   HTP_HD bool in_field(const double* bx, const double* by, int p) const {
+    const int nb = NBC ? NBC : this->nb;
     const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
     const double* V = g.vert + 2 * o;
     for (int k = 0; k < nb; ++k) {  // crossing number of each corner
@@ -244,7 +248,9 @@ struct Footprint {
   // straddle two lane polygons, or come within LANE_EPS of an edge, take the full test.
   static constexpr double LANE_EPS = 1e-9;
   mutable int lane_hint = 0;   // the lane polygon that held the last body (any holding polygon gives the result)
+  template <int NBC>
   HTP_HD bool in_one_lane(const double* bx, const double* by) const {
+    const int nb = NBC ? NBC : this->nb;
     const int nl = lane1 - lane0;
     for (int r = 0; r < nl; ++r) {
       int p = lane0 + lane_hint + r;
@@ -265,8 +271,10 @@ struct Footprint {
   }
 
   // every body edge covered by the union of the lane polygons (CCW, convex)
+  template <int NBC>
   HTP_HD bool in_lanes(const double* bx, const double* by) const {
-    if (in_one_lane(bx, by)) return true;
+    const int nb = NBC ? NBC : this->nb;
+    if (in_one_lane<NBC>(bx, by)) return true;
     const int j0 = lane0, j1 = lane1;
     for (int k = 0; k < nb; ++k) {
       const int k1 = (k + 1) == nb ? 0 : k + 1;
@@ -312,20 +320,27 @@ struct Footprint {
   // and the host build), not the double-double libm: only a collision boolean depends on it, and a last-bit
   // difference flips one only for a body within ~1e-15 m of a boundary (the oracle's numpy cos / sin are not
   // correctly rounded either).  Trajectory samples and grid indices keep htp_libm.h.
-  HTP_HD bool pose_hits(double x, double y, double yaw) const {
+  // NBC: the body's vertex count as a compile-time constant (4: the planners' rectangular bodies), so the corner
+  // arrays are indexed by constants and stay in registers; 0: the run-time count (scratch memory)
+  template <int NBC>
+  HTP_HD bool pose_hits_t(double x, double y, double yaw) const {
+    const int nb = NBC ? NBC : this->nb;
     double sn, cs;
     fm::sincos(yaw, sn, cs);
-    double bx[MAXB], by[MAXB];
+    double bx[NBC ? NBC : MAXB], by[NBC ? NBC : MAXB];
     for (int k = 0; k < nb; ++k) {
       const double vx = body[2 * k], vy = body[2 * k + 1];
       bx[k] = cs * vx + (-sn) * vy + x;
       by[k] = sn * vx + cs * vy + y;
     }
     for (int p = blk0; p < blk1; ++p)
-      if (sat_hit(bx, by, p)) return true;
-    if (field >= 0 && !in_field(bx, by, field)) return true;
-    if (lane1 > lane0 && !in_lanes(bx, by)) return true;
+      if (sat_hit<NBC>(bx, by, p)) return true;
+    if (field >= 0 && !in_field<NBC>(bx, by, field)) return true;
+    if (lane1 > lane0 && !in_lanes<NBC>(bx, by)) return true;
     return false;
+  }
+  HTP_HD bool pose_hits(double x, double y, double yaw) const {
+    return nb == 4 ? pose_hits_t<4>(x, y, yaw) : pose_hits_t<0>(x, y, yaw);
   }
 
 };

@@ -418,6 +418,9 @@ HTP_HD HTP_FI inline T& pkx(T* K, int r, int c) { return K[S * (r >= c ? r * (r 
 #ifndef HTP_BK_BATCH
 #define HTP_BK_BATCH 1
 #endif
+#ifndef HTP_BK_MULTI
+#define HTP_BK_MULTI 0
+#endif
 template <class V>
 HTP_HD HTP_FI inline V sel_opaque(V x) {
 #if defined(__HIP_DEVICE_COMPILE__) && HTP_SEL_OPAQUE
@@ -824,6 +827,105 @@ HTP_HD HTP_FI inline void bk_solve_batch(const T* K, const int* ip, double* v) {
       sel_set<n>(v, km, t1);
       const int kp = -ipk - 1;
       if (kp != kc) { const double a = sel_get<n>(v, kc), b = sel_get<n>(v, kp); sel_set<n>(v, kc, b); sel_set<n>(v, kp, a); }
+      k -= 2;
+    }
+  }
+}
+
+// bk_solve_batch for NR right-hand sides at once (HTP_BK_MULTI): the steps' pivot selects and LDS loads are shared
+// by the columns, each column sees exactly bk_solve_batch's operations.
+template <int n, int S, int NR, class T>
+HTP_HD HTP_FI inline void bk_solve_batch_multi(const T* K, const int* ip, double (*v)[n]) {
+  int k = 0;
+#pragma unroll 1
+  for (int step = 0; step < n; ++step) {          // forward: P, L, D
+    const bool act = k < n;
+    const int kc = act ? k : 0;
+    const int ipk = sel_get<n>(ip, kc);
+    const int kc1 = kc + 1 < n ? kc + 1 : kc;
+    double ca[n], cb[n];
+#pragma unroll
+    for (int r = 0; r < n; ++r) { ca[r] = K[S * (r * (r + 1) / 2 + kc)]; cb[r] = K[S * (r * (r + 1) / 2 + kc1)]; }
+    const double d11 = K[S * (kc * (kc + 1) / 2 + kc)], d21 = K[S * (kc1 * (kc1 + 1) / 2 + kc)];
+    const double d22 = K[S * (kc1 * (kc1 + 1) / 2 + kc1)];
+    if (act && ipk >= 0) {
+      const int kp = ipk;
+#pragma unroll
+      for (int c = 0; c < NR; ++c) {
+        if (kp != kc) { const double a = sel_get<n>(v[c], kc), b = sel_get<n>(v[c], kp); sel_set<n>(v[c], kc, b); sel_set<n>(v[c], kp, a); }
+        const double vk = sel_get<n>(v[c], kc);
+#pragma unroll
+        for (int r = 1; r < n; ++r) {
+          const double nv = v[c][r] - ca[r] * vk;
+          v[c][r] = (r > kc) ? nv : v[c][r];
+        }
+#pragma unroll
+        for (int j = 0; j < n; ++j) v[c][j] = (j == kc) ? v[c][j] / d11 : v[c][j];
+      }
+      k += 1;
+    } else if (act) {
+      const int kp = -ipk - 1;
+      const double det = d11 * d22 - d21 * d21;
+#pragma unroll
+      for (int c = 0; c < NR; ++c) {
+        if (kp != kc + 1) {
+          const double a = sel_get<n>(v[c], kc + 1), b = sel_get<n>(v[c], kp);
+          sel_set<n>(v[c], kc + 1, b);
+          sel_set<n>(v[c], kp, a);
+        }
+        const double vk = sel_get<n>(v[c], kc), vk1 = sel_get<n>(v[c], kc + 1);
+#pragma unroll
+        for (int r = 2; r < n; ++r) {
+          const double nv = v[c][r] - (ca[r] * vk + cb[r] * vk1);
+          v[c][r] = (r > kc + 1) ? nv : v[c][r];
+        }
+        const double b1 = vk, b2 = vk1;
+        sel_set<n>(v[c], kc, (d22 * b1 - d21 * b2) / det);
+        sel_set<n>(v[c], kc + 1, (-d21 * b1 + d11 * b2) / det);
+      }
+      k += 2;
+    }
+  }
+  k = n - 1;
+#pragma unroll 1
+  for (int step = 0; step < n; ++step) {          // backward: L', P'
+    const bool act = k >= 0;
+    const int kc = act ? k : 0;
+    const int ipk = sel_get<n>(ip, kc);
+    const int km = kc >= 1 ? kc - 1 : 0;
+    double ca[n], cm[n];
+#pragma unroll
+    for (int r = 0; r < n; ++r) { ca[r] = K[S * (r * (r + 1) / 2 + kc)]; cm[r] = K[S * (r * (r + 1) / 2 + km)]; }
+    if (act && ipk >= 0) {
+      const int kp = ipk;
+#pragma unroll
+      for (int c = 0; c < NR; ++c) {
+        double t = sel_get<n>(v[c], kc);
+#pragma unroll
+        for (int r = 1; r < n; ++r) {
+          const double nt = t - ca[r] * v[c][r];
+          t = (r > kc) ? nt : t;
+        }
+        sel_set<n>(v[c], kc, t);
+        if (kp != kc) { const double a = sel_get<n>(v[c], kc), b = sel_get<n>(v[c], kp); sel_set<n>(v[c], kc, b); sel_set<n>(v[c], kp, a); }
+      }
+      k -= 1;
+    } else if (act) {
+      const int kp = -ipk - 1;
+#pragma unroll
+      for (int c = 0; c < NR; ++c) {
+        double t = sel_get<n>(v[c], kc), t1 = sel_get<n>(v[c], km);
+#pragma unroll
+        for (int r = 1; r < n; ++r) {
+          const double nt = t - ca[r] * v[c][r];
+          const double nt1 = t1 - cm[r] * v[c][r];
+          t = (r > kc) ? nt : t;
+          t1 = (r > kc) ? nt1 : t1;
+        }
+        sel_set<n>(v[c], kc, t);
+        sel_set<n>(v[c], km, t1);
+        if (kp != kc) { const double a = sel_get<n>(v[c], kc), b = sel_get<n>(v[c], kp); sel_set<n>(v[c], kc, b); sel_set<n>(v[c], kp, a); }
+      }
       k -= 2;
     }
   }
@@ -1834,6 +1936,17 @@ struct ObcaSolver {
 #endif
 #if defined(HTP_LPROF) && HTP_LPROF == 2
       lp2_t = c.clock();
+#endif
+#if HTP_BK_MULTI && HTP_BK_BATCH
+      if constexpr (NRHS > 1) {
+        double v[NRHS][NL];
+#pragma unroll
+        for (int k = 0; k < NRHS; ++k) col(k, v[k], false);
+        bk_solve_batch_multi<NL, 64, NRHS>(K, ip, v);
+#pragma unroll
+        for (int k = 0; k < NRHS; ++k) col(k, v[k], true);
+        return;
+      }
 #endif
 #pragma unroll
       for (int k = 0; k < NRHS; ++k) {
