@@ -20,6 +20,7 @@
 #     fx:NAME,..:variant,..   tools/fixture_probe.py (oracle fixtures under A/B variants)
 #     counters  rocprofv3 --list-avail (the PMC counter names of this box)
 #     tail      tools/tail_probe.py on config D 32768 (per-problem cycles -> TAG_tail_D.npz for scale_projection.py)
+#     tailE     the same on config E 4096 (which solves reach the 20 s limit, at what cost per iteration)
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
@@ -91,6 +92,8 @@ for S in "$@"; do
              n=$(echo $grp | cut -c1-12 | tr ' ' '_')
              run hapmc_$n 180 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${T}_hapmc_$n -o pmc -- python3 tools/bench_hastar.py --no-cpu --steps 1 --warmup 0
            done ;;
+    tailE) run tailgenE 300 python -u bench.py --config E --batch 4096 --gen-only --cache /tmp/htp_instcache
+           run tailE 600 python -u tools/tail_probe.py E 4096 /tmp/htp_instcache gpurun_out/${T}_tail_E.npz ;;
     tail) run tailgen 300 python -u bench.py --gen-only --cache /tmp/htp_instcache
           run tail 600 python -u tools/tail_probe.py D 32768 /tmp/htp_instcache gpurun_out/${T}_tail_D.npz ;;
     *) echo "unknown step $S"; exit 2 ;;
