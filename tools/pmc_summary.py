@@ -79,8 +79,8 @@ def main():
     sq, smeta = rows(base, tag, "sq")
     bl_s = bench_line(base, tag, "sq")
     it_s = bl_s["solver"]["mean_iters"] * bl_s["config"]["global_batch"] * bl_s["steps"]
-    mf = {"workload": cfg, "solver_sha": sha, "kernel": smeta.get("kernel"), "counters": sq,
-          "launch_iterations": it_s}
+    mf = {"workload": cfg, "solver_sha": sha, "kernel": smeta.get("kernel"), "binary": bl_s.get("binary"),
+          "counters": sq, "launch_iterations": it_s}
     if sq:
         mf["mfma_f64_per_problem_iter"] = sq.get("SQ_INSTS_VALU_MFMA_F64", 0.0) / it_s
         mf["mfma_mops_f64_per_problem_iter"] = sq.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0) / it_s
