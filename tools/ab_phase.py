@@ -53,7 +53,7 @@ for rnd in range(2):
                         cyc[:, 1].sum() / sw, cyc[:, 3].sum() / sw, cyc[:, 5].sum() / sw, cyc[:, 6].sum() / sw,
                         sw / max(1, r.iterations.sum()))
             if "prof" in k and "kprof" not in k:   # HTP_PROF_ON: stage-chain sub-steps (factor 1/3/5, solve 6/7)
-                nm = ["p0", "fac_mfma", "p2", "fac_chol", "total", "fac_tail", "solve_bwd*", "solve_fwd"]
+                nm = ["fac_relax", "fac_mfma", "fac_pn_store", "fac_chol", "total", "fac_sym", "solve_bwd*", "solve_fwd"]
             line += " | " + " ".join(f"{nm[j]} {cyc[:, j].sum() / tot:.3f}" for j in (0, 1, 2, 3, 5, 6, 7))
             line += " | per-iter cycles %.3g" % (cyc[:, 4] / np.maximum(1, r.iterations)).mean()
         print(line, flush=True)
