@@ -36,6 +36,7 @@
 
 #include "dubins_core.h"
 #include "rs_core.h"
+#include "../../include/htp.h"
 
 #if defined(__clang__)
 #pragma clang fp contract(off)
@@ -52,6 +53,8 @@ constexpr int MAXTRAJ = 64;   // poses per motion primitive (round(L/res) + 1)
 // search length 1.5 m at 0.1 m); 512 keeps a search's LDS at ~21 KB, 7 resident searches per CU instead of 4.
 constexpr int TRAJCAP = 512;
 constexpr int MAXJ = 32;      // lane polygons
+static_assert(MAXB == HTP_HA_MAX_BODY && MAXMOT == HTP_HA_MAX_MOTIONS && MAXTRAJ == HTP_HA_MAX_POSES &&
+              TRAJCAP == HTP_HA_TRAJ_CAP && MAXJ == HTP_HA_MAX_LANES, "include/htp.h documents these limits");
 constexpr int MAXCHAIN = 1 << 20;
 constexpr double PI = 3.141592653589793;
 
@@ -76,6 +79,56 @@ struct Geo {
   const double* guide;      // [nguide][4] x, y, yaw, s
   const double* motion;     // [nmotion][2] steer, direction
 };
+
+// A batch's pools (htp.h htp_hastar_batch) as the search reads them.
+struct Pools {
+  const double* params;
+  const int32_t* desc;
+  Geo g;
+  int32_t npoly, nvert, nguide, nmotion;
+};
+
+// The polygon table's ranges (the searches trust poly_off): checked once per batch on the host.
+inline bool poly_table_ok(const int32_t* poly_off, int npoly, int nvert) {
+  for (int p = 0; p < npoly; ++p)
+    if (poly_off[p] < 0 || poly_off[p + 1] < poly_off[p] || poly_off[p + 1] > nvert) return false;
+  return true;
+}
+
+// Per-search shape checks the search relies on (descriptor ranges, body vertex count <= MAXB, lane count <= MAXJ,
+// motion count <= MAXMOT, positive resolutions, max_nodes <= the workspace's cap).  Every search length L (the
+// default and each lane's) must give n = rint(L / res) with 1 <= n, n + 1 <= MAXTRAJ and nmot (n + 1) <= TRAJCAP:
+// one expansion's rollouts live in LDS (King's 14 motions: n + 1 <= 36, i.e. L <= 35 res).  A search failing any
+// check ends HTP_HA_BAD_INPUT on the device and on the host build alike.
+HTP_HD inline bool valid_search(const Pools& P, const double* prm, const int32_t* d, int max_nodes_cap) {
+  auto poly_ok = [&](int p) { return p >= 0 && p < P.npoly; };
+  if (!poly_ok(d[D_BODY])) return false;
+  const int nb = P.g.poly_off[d[D_BODY] + 1] - P.g.poly_off[d[D_BODY]];
+  if (nb < 3 || nb > MAXB) return false;
+  if (d[D_BLK0] < 0 || d[D_BLK1] < d[D_BLK0] || d[D_BLK1] > P.npoly) return false;
+  if (d[D_LANE0] < 0 || d[D_LANE1] <= d[D_LANE0] || d[D_LANE1] > P.npoly || d[D_LANE1] - d[D_LANE0] > MAXJ) return false;
+  if (d[D_FIELD] != -1 && !poly_ok(d[D_FIELD])) return false;
+  if (d[D_GUIDE0] < 0 || d[D_GUIDE1] <= d[D_GUIDE0] || d[D_GUIDE1] > P.nguide) return false;
+  if (d[D_MOT0] < 0 || d[D_MOT1] <= d[D_MOT0] || d[D_MOT1] > P.nmotion || d[D_MOT1] - d[D_MOT0] > MAXMOT) return false;
+  if (d[D_KING] != 0 && d[D_KING] != 1) return false;
+  const double res = prm[P_RES];
+  if (!(res > 0) || !(prm[P_YAWRES] > 0) || !(prm[P_WB] > 0) || !(prm[P_CURV] > 0)) return false;
+  const double mn = prm[P_MAXNODES];
+  if (!(mn >= 0) || mn > (double)max_nodes_cap) return false;
+  const int nmot = d[D_MOT1] - d[D_MOT0];
+  auto len_ok = [&](double L) {
+    const double n = rint(L / res);
+    return n >= 1 && n + 1 <= MAXTRAJ && (double)nmot * (n + 1) <= (double)TRAJCAP;
+  };
+  if (!len_ok(prm[P_DEFLEN])) return false;
+  for (int p = d[D_LANE0]; p < d[D_LANE1]; ++p)
+    if (!len_ok(P.g.lane_len[p])) return false;
+  for (int p = d[D_BLK0]; p < d[D_BLK1]; ++p)
+    if (P.g.poly_off[p + 1] - P.g.poly_off[p] < 1) return false;
+  for (int p = d[D_LANE0]; p < d[D_LANE1]; ++p)
+    if (P.g.poly_off[p + 1] - P.g.poly_off[p] < 3) return false;
+  return true;
+}
 
 struct Node {  // 64 B
   double x, y, yaw, cost, curv;

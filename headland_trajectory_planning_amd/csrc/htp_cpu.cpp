@@ -161,6 +161,12 @@ extern "C" int htp_cpu_hastar_range(const htp_hastar_batch* in, htp_hastar_resul
                                     int nthreads) {
   if (!in || !out || first < 0 || count < 0 || first + count > in->batch || in->max_nodes_cap < 0) return -1;
   using namespace htp::ha;
+  if (!in->params || !in->desc || !in->poly_off || !in->vertices || !in->lane_len || !in->guide || !in->motions ||
+      in->npoly < 1 || in->nvert < 1 || in->nguide < 1 || in->nmotion < 1 || in->cap_path < 0 ||
+      !poly_table_ok(in->poly_off, in->npoly, in->nvert))
+    return -1;
+  const Pools P{in->params, in->desc, Geo{in->poly_off, in->vertices, in->lane_len, in->guide, in->motions},
+                in->npoly, in->nvert, in->nguide, in->nmotion};
   if (nthreads <= 0) nthreads = omp_get_max_threads();
   const int64_t cn = 4 + (int64_t)(in->max_nodes_cap + 1) * MAXMOT + 4;
   int64_t cs = 1;
@@ -180,10 +186,19 @@ extern "C" int htp_cpu_hastar_range(const htp_hastar_batch* in, htp_hastar_resul
       const int32_t* d = in->desc + b * HTP_HA_NDESC;
       HostLane c;
       Work w{nodes.data(), slots.data(), hval.data(), hslot.data(), (int32_t)cn, (int32_t)cs, dub.data(), CAP_DUB};
-      Search<HostLane> S(c, prm, d, g, w, *sh);
       Out o{};
-      S.run(o, nullptr, 0);
       int n_path = 0;
+      if (!valid_search(P, prm, d, in->max_nodes_cap)) {   // as the device kernel: the search is not run
+        o.status = ST_BAD_INPUT;
+        if (out->status) out->status[b] = o.status;
+        if (out->counter) out->counter[b] = 0;
+        if (out->n_path) out->n_path[b] = 0;
+        if (out->n_expanded) out->n_expanded[b] = 0;
+        if (out->n_pose) out->n_pose[b] = 0;
+        continue;
+      }
+      Search<HostLane> S(c, prm, d, g, w, *sh);
+      S.run(o, nullptr, 0);
       if (out->x && (o.status == ST_FOUND || o.status == ST_NO_PATH || o.status == ST_MAX_NODES)) {
         const int64_t off = b * in->cap_path;
         int st = o.status;

@@ -18,12 +18,6 @@ using namespace htp::ha;
 
 namespace {
 
-struct Pools {
-  const double* params;
-  const int32_t* desc;
-  Geo g;
-  int32_t npoly, nvert, nguide, nmotion;
-};
 
 struct Sizes {
   int32_t cap_node, cap_slot;
@@ -58,38 +52,6 @@ HTP_HD inline Work work_of(char* base, const Sizes& z, int b) {
   return w;
 }
 
-// Shape checks the kernel relies on (polygon / guide / motion ranges, fixed capacities).
-__device__ bool valid(const Pools& P, const double* prm, const int32_t* d, int max_nodes_cap) {
-  auto poly_ok = [&](int p) { return p >= 0 && p < P.npoly; };
-  if (!poly_ok(d[D_BODY])) return false;
-  const int nb = P.g.poly_off[d[D_BODY] + 1] - P.g.poly_off[d[D_BODY]];
-  if (nb < 3 || nb > MAXB) return false;
-  if (d[D_BLK0] < 0 || d[D_BLK1] < d[D_BLK0] || d[D_BLK1] > P.npoly) return false;
-  if (d[D_LANE0] < 0 || d[D_LANE1] <= d[D_LANE0] || d[D_LANE1] > P.npoly || d[D_LANE1] - d[D_LANE0] > MAXJ) return false;
-  if (d[D_FIELD] != -1 && !poly_ok(d[D_FIELD])) return false;
-  if (d[D_GUIDE0] < 0 || d[D_GUIDE1] <= d[D_GUIDE0] || d[D_GUIDE1] > P.nguide) return false;
-  if (d[D_MOT0] < 0 || d[D_MOT1] <= d[D_MOT0] || d[D_MOT1] > P.nmotion || d[D_MOT1] - d[D_MOT0] > MAXMOT) return false;
-  if (d[D_KING] != 0 && d[D_KING] != 1) return false;
-  for (int p = 0; p < P.npoly; ++p) (void)p;
-  const double res = prm[P_RES];
-  if (!(res > 0) || !(prm[P_YAWRES] > 0) || !(prm[P_WB] > 0) || !(prm[P_CURV] > 0)) return false;
-  const double mn = prm[P_MAXNODES];
-  if (!(mn >= 0) || mn > (double)max_nodes_cap) return false;
-  // every search length must give 1 <= round(L/res), round(L/res)+1 <= MAXTRAJ and nmot (round(L/res)+1) <= TRAJCAP
-  const int nmot = d[D_MOT1] - d[D_MOT0];
-  auto len_ok = [&](double L) {
-    const double n = rint(L / res);
-    return n >= 1 && n + 1 <= MAXTRAJ && (double)nmot * (n + 1) <= (double)TRAJCAP;
-  };
-  if (!len_ok(prm[P_DEFLEN])) return false;
-  for (int p = d[D_LANE0]; p < d[D_LANE1]; ++p)
-    if (!len_ok(P.g.lane_len[p])) return false;
-  for (int p = d[D_BLK0]; p < d[D_BLK1]; ++p)
-    if (P.g.poly_off[p + 1] - P.g.poly_off[p] < 1) return false;
-  for (int p = d[D_LANE0]; p < d[D_LANE1]; ++p)
-    if (P.g.poly_off[p + 1] - P.g.poly_off[p] < 3) return false;
-  return true;
-}
 
 // One instantiation per motion type (MODE 1 King: Reeds-Shepp goal shots,
 // MODE 0 Pawn: Dubins + spline); each launch covers the whole batch and a
@@ -112,7 +74,7 @@ __global__ __launch_bounds__(64) void hastar_kernel(Pools P, int batch, int max_
   DevWave c{(int)threadIdx.x, nullptr, nullptr};
   Out o{};
   int n_path = 0;
-  if (!valid(P, prm, d, max_nodes_cap)) {
+  if (!valid_search(P, prm, d, max_nodes_cap)) {
     o.status = ST_BAD_INPUT;
   } else {
     Work w = work_of(ws, z, b);
@@ -193,9 +155,7 @@ int htp_hastar_search_batch(htp_ctx* ctx, const htp_hastar_batch* in, htp_hastar
   if (check_in(ctx, in, out)) return -1;
   if (in->batch == 0) return 0;
   // host-side range check of the polygon table (the kernel trusts poly_off)
-  for (int p = 0; p < in->npoly; ++p)
-    if (in->poly_off[p] < 0 || in->poly_off[p + 1] < in->poly_off[p] || in->poly_off[p + 1] > in->nvert)
-      return fail(ctx, "hastar: poly_off out of range");
+  if (!poly_table_ok(in->poly_off, in->npoly, in->nvert)) return fail(ctx, "hastar: poly_off out of range");
   HIPCHK(hipSetDevice(ctx->device));
   const int64_t B = in->batch;
   const int64_t cp = in->cap_path, cl = out->expanded ? in->cap_log : 0;

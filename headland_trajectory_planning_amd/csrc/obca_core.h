@@ -158,6 +158,7 @@ HTP_HD inline double dabs(double a) { return a < 0 ? -a : a; }
 constexpr double HTP_INF = __builtin_huge_val();
 
 #ifdef HTP_TRACE_ON
+#include <cstdio>
 #define HTP_TRACE(...) do { if (c.lane == 0) printf(__VA_ARGS__); } while (0)
 #else
 #define HTP_TRACE(...) do { } while (0)
@@ -5929,7 +5930,7 @@ struct ObcaSolver {
       grad_lag_into(gl);
       Err emu;  // errors at the current mu, from the same sweeps (the first barrier test below)
       Err e0 = errors(gl, 0.0, mu, &emu);
-      HTP_TRACE("[trace] it %d%s err dual=%g comp=%g prim=%g mu=%g\n", it, rs ? " R" : "", e0.dual, e0.comp, e0.prim_nlp, mu);
+      HTP_TRACE("[trace] it %d%s err dual=%.17g comp=%.17g prim=%.17g mu=%.17g\n", it, rs ? " R" : "", e0.dual, e0.comp, e0.prim_nlp, mu);
       nlp_err = dmax(dmax(e0.dual / e0.s_d, e0.prim_nlp), e0.comp / e0.s_c);
       const double uv = unscaled_viol();
       const double sfm = rs ? 1.0 : sf;

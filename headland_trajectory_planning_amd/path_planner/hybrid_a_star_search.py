@@ -60,6 +60,31 @@ def lower_problem(start_pose, goal_pose, config_environment, car_model, search_h
         motions=motion_steers(car_model.MAX_STEER, yaw_resolution, motion_type))
 
 
+# Per-search limits of the device search (include/htp.h HTP_HA_MAX_*, hastar_core.h valid_search).  The reference
+# has none; its planners' settings stay far inside them (King: 14 motions x 16 poses of 512).
+MAX_BODY, MAX_LANES, MAX_MOTIONS, MAX_POSES, TRAJ_CAP = 8, 32, 16, 64, 512
+
+
+def check_limits(p):
+    """Raise ValueError, naming the limit, for a lowered search the device would reject (HTP_HA_BAD_INPUT): every
+    search length L (the default and each lane's) needs n = rint(L / res) >= 1 with n + 1 <= MAX_POSES poses per
+    motion primitive and nmotions * (n + 1) <= TRAJ_CAP (one expansion's rollouts are held in LDS)."""
+    nmot = len(p["motions"])
+    if not 1 <= nmot <= MAX_MOTIONS:
+        raise ValueError(f"[HA*] {nmot} motion primitives; the device search takes 1..{MAX_MOTIONS}")
+    nb = len(_native._clean_ring(p["body"]))
+    if not 3 <= nb <= MAX_BODY:
+        raise ValueError(f"[HA*] body polygon with {nb} vertices; the device search takes 3..{MAX_BODY}")
+    if not 1 <= len(p["lanes"]) <= MAX_LANES:
+        raise ValueError(f"[HA*] {len(p['lanes'])} lane polygons; the device search takes 1..{MAX_LANES}")
+    for L in [p["default_search_length"]] + [float(v) for v in p["search_lengths"]]:
+        n = int(np.rint(L / p["res"]))
+        if n < 1 or n + 1 > MAX_POSES or nmot * (n + 1) > TRAJ_CAP:
+            raise ValueError(f"[HA*] search length {L} at resolution {p['res']} gives {n + 1} poses per motion "
+                             f"primitive x {nmot} primitives; the device search holds at most {MAX_POSES} per "
+                             f"primitive and {TRAJ_CAP} per expansion (include/htp.h HTP_HA_TRAJ_CAP)")
+
+
 _CTX = None
 
 
@@ -73,6 +98,8 @@ def _context():
 def search_lowered(problems, ctx=None, cap_path=4096):
     """Run lowered problems on the GPU -> list of dicts (xs, ys, yaws, dirs, ks, counter, status, expanded)."""
     ctx = ctx or _context()
+    for p in problems:
+        check_limits(p)
     packed = _native.HastarPacked(problems, cap_path=cap_path)
     res = ctx.hastar(packed)
     if np.any(res.n_path > cap_path):

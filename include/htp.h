@@ -272,9 +272,21 @@ enum {
   HTP_HA_START_GOAL_BLOCKED = 3,
   HTP_HA_RS_ERROR = 4,         /* the reference raises inside reeds_shepp.calc_all_paths */
   HTP_HA_CAPACITY = 5,         /* node pool exhausted (cannot happen with the library's sizing) */
-  HTP_HA_BAD_INPUT = 6,
+  HTP_HA_BAD_INPUT = 6,        /* a per-search shape check failed (see the limits below); the search is not run */
   HTP_HA_BACKTRACK = 7         /* the reference raises KeyError while backtracking */
 };
+/* Per-search limits (hastar_core.h valid_search; a search outside them ends HTP_HA_BAD_INPUT on the device and in
+ * the host build alike): body polygon 3..HTP_HA_MAX_BODY vertices, at most HTP_HA_MAX_LANES lane polygons and
+ * HTP_HA_MAX_MOTIONS motion primitives, and for every search length L (HTP_HA_P_DEFLEN and each lane's lane_len)
+ * n = rint(L / HTP_HA_P_RES) with 1 <= n, n + 1 <= HTP_HA_MAX_POSES and nmotions * (n + 1) <= HTP_HA_TRAJ_CAP:
+ * one expansion's rollouts are held in LDS.  The reference has no such limit; its planners' settings need at most
+ * 14 x 16 = 224 (King, search length 1.5 m at 0.1 m).  King's 14 motions allow n + 1 <= 36 poses per primitive,
+ * i.e. L <= 35 res (3.5 m at 0.1 m). */
+#define HTP_HA_MAX_BODY 8
+#define HTP_HA_MAX_LANES 32
+#define HTP_HA_MAX_MOTIONS 16
+#define HTP_HA_MAX_POSES 64
+#define HTP_HA_TRAJ_CAP 512
 
 typedef struct {
   int32_t batch;

@@ -666,7 +666,8 @@ class _Ipm:
             e0 = self.errors(it, c, d, Jc, Jd, 0.0)
             nlp_err = max(e0["dual"] / e0["s_d"], e0["prim_nlp"], e0["comp"] / e0["s_c"])
             uviol = p.unscaled_viol(it.x, c, d)
-            self.log.append(dict(it=k, resto=p.is_resto, mu=self.mu, err=nlp_err, theta=self.theta(c, d, it.s)))
+            self.log.append(dict(it=k, resto=p.is_resto, mu=self.mu, err=nlp_err, theta=self.theta(c, d, it.s),
+                                 dual=e0["dual"], comp=e0["comp"], prim=e0["prim_nlp"]))
             # ---- convergence check
             if p.is_resto:
                 st = self.resto_check(it, first)

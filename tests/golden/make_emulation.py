@@ -7,6 +7,7 @@ host build (HostLane, the oracle's summation order) ends where the oracle ends -
 summation order and nothing else.
 
     python tests/golden/make_emulation.py D347 E84 E6 P19     -> tests/golden/emulation/<name>.npz
+    python tests/golden/make_emulation.py short               -> tests/golden/emulation/short_solves.npz
 """
 import os
 import sys
@@ -40,9 +41,57 @@ def run(name):
     return f"{name}: status {r.status[0]} it {r.iterations[0]} resto {r.n_resto[0]} ({time.time() - t:.0f} s)"
 
 
+def short_groups():
+    """tests/test_gpu_emulation.py::test_short_solves_equal_the_emulation's launches (one shape per launch)."""
+    from headland_trajectory_planning_amd import synth
+    insts = [synth.config_instance("D", p) for p in range(3)] + [synth.config_instance("C", 0),
+                                                                  synth.config_instance("A", 1)]
+    W = np.diag([10.0, 0.1])
+    insts += [synth.make_instance(p, N=12, M=2, implement="mower", W=W) for p in (0, 3)]   # restoration phases
+    return [[insts[k] for k in (0, 1, 2)], [insts[3]], [insts[4]], insts[5:]]
+
+
+def emu_key():
+    """Hash of every source the emulation's doubles depend on: the solver core (_native.core_sha) and the
+    emulation itself (csrc/emu_wave.h, csrc/htp_emusim.cpp, the MFMA model in csrc/wave_ctx.h)."""
+    import hashlib
+    from headland_trajectory_planning_amd import _native
+    h = hashlib.sha256(_native.core_sha().encode())
+    for f in ("emu_wave.h", "htp_emusim.cpp"):
+        with open(os.path.join(ROOT, "headland_trajectory_planning_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def group_hash(group):
+    from make_oracle_screen import inst_hash
+    import hashlib
+    return hashlib.sha256("".join(inst_hash(i) for i in group).encode()).hexdigest()[:16]
+
+
+def run_short():
+    """The short solves' emulation, cached (the live run takes minutes of host time on the GPU box):
+    tests/golden/emulation/short_solves.npz, keyed by emu_key() and each launch's instance hash."""
+    import _hostsim as H
+    t = time.time()
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    out = {"key": emu_key()}
+    for g, group in enumerate(short_groups()):
+        r = H.solve_emusim(group)
+        out.update({f"g{g}_hash": group_hash(group), f"g{g}_x": r.x, f"g{g}_status": r.status,
+                    f"g{g}_iters": r.iterations, f"g{g}_n_resto": r.n_resto, f"g{g}_objective": r.objective})
+    out["ngroups"] = len(short_groups())
+    out["seconds"] = time.time() - t
+    np.savez(os.path.join(OUT, "short_solves.npz"), **out)
+    return f"short solves: {out['ngroups']} launches emulated ({time.time() - t:.0f} s), key {out['key']}"
+
+
 if __name__ == "__main__":
     import _hostsim as H
     H.build_emusim()
+    if sys.argv[1:] == ["short"]:
+        print(run_short(), flush=True)
+        sys.exit(0)
     import multiprocessing as mp
     with mp.Pool(min(3, len(sys.argv) - 1)) as pool:
         for line in pool.imap_unordered(run, sys.argv[1:]):

@@ -28,7 +28,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
-OUT = os.path.join(ROOT, "tests", "golden", "obca_full")
+OUT = os.environ.get("HTP_GOLDEN_OUT", os.path.join(ROOT, "tests", "golden", "obca_full"))
 
 CASES = ["A:0", "A:1", "A:2", "B:0", "B:1", "B:9", "D:0", "D:33", "D:971", "C:0", "C:1", "C:2", "C:47", "E:0", "E:1",
          "E:12"]

@@ -15,8 +15,8 @@ SX VM calls in the reference's own solve) instead of numpy's AVX-512 kernels:
     python tests/golden/make_witness.py E12:glibc E54:glibc  -> tests/golden/witness/<name>_libm.npz
 
 Input-rounding witnesses: the same oracle on the fixture's instance with ONE input double moved by one ulp
-(the first initial-guess state x_0 component K, np.nextafter), i.e. an instance the reference cannot tell
-apart from the fixture's after its own float parsing and arithmetic:
+(init_traj[tests/_neighbours.ulp_cell(K, N)], np.nextafter; each file stores the moved (row, col) as `cell`),
+i.e. an instance the reference cannot tell apart from the fixture's after its own float parsing and arithmetic:
 
     python tests/golden/make_witness.py E12:ulp0 E12:ulp1   -> tests/golden/witness/<name>_ulp<K>.npz
 """
@@ -29,10 +29,17 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
-OUT = os.path.join(ROOT, "tests", "golden", "witness")
+OUT = os.environ.get("HTP_WITNESS_OUT", os.path.join(ROOT, "tests", "golden", "witness"))
 
 
 def run(name):
+    try:
+        return _run(name)
+    except Exception as e:  # noqa: BLE001 -- one run's failure must not end the others (pool)
+        return f"{name}: ERROR {type(e).__name__}: {e}"
+
+
+def _run(name):
     from oracle.ipm import IpoptRestatement
     t = time.time()
     if name.endswith(":glibc"):
@@ -102,10 +109,8 @@ def run_ulp(name, k, t):
     from oracle.structured import StructuredKKT
     g = np.load(os.path.join(ROOT, "tests", "golden", "obca_full", f"{name}.npz"))
     inst = load_instance(g)
-    tr = np.array(inst["init_traj"], dtype=np.float64)
-    row, col = (k // 2, (k % 2)) if k < 4 else ((1 + k, 0) if k < 8 else (k - 4, 1))
-    tr[row, col] = np.nextafter(tr[row, col], np.inf)
-    inst = dict(inst, init_traj=tr)
+    from _neighbours import neighbour
+    inst, (row, col) = neighbour(inst, k)
     nlp = ObcaNLP(inst)
     N = int(g["N"])
     a = {"x": g["states"], "status": int(g["status"]), "iters": int(g["iters"]), "n_resto": int(g["n_resto"])}
@@ -115,7 +120,7 @@ def run_ulp(name, k, t):
     np.savez(os.path.join(OUT, f"{name}_ulp{k}.npz"), orders=np.array(orders),
              states_a=a["x"][:5 * N], status_a=a["status"], iters_a=a["iters"], n_resto_a=a["n_resto"],
              states_b=b["x"][:5 * N], status_b=b["status"], iters_b=b["iters"], n_resto_b=b["n_resto"],
-             seconds=time.time() - t)
+             f_b=b["f"], cell=np.array([row, col]), seconds=time.time() - t)
     d = float(np.max(np.abs(a["x"][:5 * N] - b["x"][:5 * N])))
     return (f"{name} ulp{k}: fixture status {a['status']} it {a['iters']} resto {a['n_resto']} | +1 ulp status "
             f"{b['status']} it {b['iters']} resto {b['n_resto']} | max state diff {d:.3g} ({time.time() - t:.0f} s)")
@@ -123,6 +128,6 @@ def run_ulp(name, k, t):
 
 if __name__ == "__main__":
     import multiprocessing as mp
-    with mp.Pool(min(4, len(sys.argv) - 1)) as pool:
+    with mp.Pool(min(int(os.environ.get("HTP_PROCS", "4")), len(sys.argv) - 1)) as pool:
         for line in pool.imap_unordered(run, sys.argv[1:]):
             print(line, flush=True)

@@ -44,3 +44,17 @@ def test_e54_status_split():
     init_traj[0, 1] one ulp up: the oracle converges (Solve_Succeeded after 652 / 2 phases)."""
     w = np.load(os.path.join(W, "E54_ulp1.npz"))
     assert int(w["status_a"]) == 7 and int(w["status_b"]) == 0
+
+
+def test_ulp_witnesses_record_the_moved_cell():
+    """Every one-ulp witness stores the init_traj cell it moved, and it is the one tests/_neighbours.ulp_cell
+    assigns to its index (the mapping the GPU neighbourhood test solves with)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from _neighbours import ulp_cell
+    files = sorted(f for f in os.listdir(W) if "_ulp" in f)
+    assert files
+    for f in files:
+        w = np.load(os.path.join(W, f))
+        k = int(f[:-4].split("_ulp")[1])
+        assert tuple(int(v) for v in w["cell"]) == ulp_cell(k, len(w["states_a"]) // 5), f

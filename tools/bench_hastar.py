@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--max-nodes", type=int, default=400)
+    ap.add_argument("--unique", type=int, default=512,
+                    help="distinct collision-free scenarios, repeated to --batch (round 5's workload: 512)")
     ap.add_argument("--cpu-sample", type=int, default=512)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiled runs)")
     ap.add_argument("--lib", default="", help="A/B: libhtp_<name>.so instead of libhtp.so")
@@ -43,7 +45,7 @@ def main():
     # 1-node search on the GPU (the blocked test runs before the first expansion), outside the timing.
     lib = _native.load(_native.LIB_PATH.replace("libhtp.so", f"libhtp_{args.lib}.so")) if args.lib else None
     ctx = _native.Context(0, lib=lib) if lib else _native.Context(0)
-    want = min(args.batch, 512)
+    want = min(args.batch, args.unique)
     uniq, seed, skipped = [], 0, 0
     while len(uniq) < want:
         seeds = list(range(seed, seed + 2 * want))
