@@ -323,7 +323,12 @@ struct Footprint {
     return false;
   }
 
-  // every body edge covered by the union of the lane polygons (CCW, convex)
+  // every body edge covered by the union of the lane polygons (CCW, convex).  Per edge A -> B each lane polygon
+  // clips the segment to a parameter interval [l, h] (the same expressions as before); the edge is covered iff the
+  // chain of intervals reachable from 0 reaches 1.  The reach is the least fixpoint of reach = max(reach, h over
+  // intervals with l <= reach), found by re-clipping the polygons each pass instead of keeping the intervals in a
+  // per-lane array (a run-time-indexed array lives in scratch memory on the device): the same fixpoint, so the same
+  // boolean as the sorted sweep of the reference's shapely union, and no private memory.
   template <int NBC>
   HTP_HD bool in_lanes(const double* bx, const double* by) const {
     const int nb = NBC ? NBC : this->nb;
@@ -332,37 +337,27 @@ struct Footprint {
     for (int k = 0; k < nb; ++k) {
       const int k1 = (k + 1) == nb ? 0 : k + 1;
       const double Ax = bx[k], Ay = by[k], Bx = bx[k1], By = by[k1];
-      double lo[MAXJ], hi[MAXJ];
-      int n = 0;
-      for (int p = j0; p < j1; ++p) {
-        const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
-        const double* V = g.vert + 2 * o;
-        double l = 0.0, h = 1.0;
-        bool dead = false;
-        for (int i = 0; i < m; ++i) {
-          const int j = (i + 1) == m ? 0 : i + 1;
-          const double vx = V[2 * i], vy = V[2 * i + 1];
-          const double ex = V[2 * j] - vx, ey = V[2 * j + 1] - vy;
-          const double c0 = ex * (Ay - vy) - ey * (Ax - vx);
-          const double c1 = ex * (By - Ay) - ey * (Bx - Ax);
-          if (c1 > 0) { const double t = -c0 / c1; if (t > l) l = t; }
-          else if (c1 < 0) { const double t = -c0 / c1; if (t < h) h = t; }
-          else if (c0 < 0) dead = true;
-        }
-        if (!dead && l <= h) { lo[n] = l; hi[n] = h; ++n; }
-      }
-      // == sorted sweep "no gap, reach >= 1" (intervals lie in [0, 1])
       double reach = 0.0;
-      bool grew = true;
-      while (grew) {
-        grew = false;
-        for (int i = 0; i < n; ++i) {
-          if (lo[i] <= reach) {
-            if (hi[i] > reach) reach = hi[i];
-            lo[i] = 2.0;  // consumed
-            grew = true;
+      for (int pass = 0; pass <= j1 - j0 && reach < 1.0; ++pass) {
+        bool grew = false;
+        for (int p = j0; p < j1; ++p) {
+          const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
+          const double* V = g.vert + 2 * o;
+          double l = 0.0, h = 1.0;
+          bool dead = false;
+          for (int i = 0; i < m; ++i) {
+            const int j = (i + 1) == m ? 0 : i + 1;
+            const double vx = V[2 * i], vy = V[2 * i + 1];
+            const double ex = V[2 * j] - vx, ey = V[2 * j + 1] - vy;
+            const double c0 = ex * (Ay - vy) - ey * (Ax - vx);
+            const double c1 = ex * (By - Ay) - ey * (Bx - Ax);
+            if (c1 > 0) { const double t = -c0 / c1; if (t > l) l = t; }
+            else if (c1 < 0) { const double t = -c0 / c1; if (t < h) h = t; }
+            else if (c0 < 0) dead = true;
           }
+          if (!dead && l <= h && l <= reach && h > reach) { reach = h; grew = true; }
         }
+        if (!grew) break;
       }
       if (!(reach >= 1.0)) return false;
     }

