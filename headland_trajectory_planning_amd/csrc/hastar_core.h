@@ -45,6 +45,12 @@
 namespace htp {
 namespace ha {
 
+// in_lanes: keep each lane polygon's clip interval in a per-lane array and sweep it (1: round 5; the array is
+// run-time indexed, so it lives in scratch memory) or re-clip the polygons on every sweep pass (0: no private array)
+#ifndef HTP_HA_LANE_ARRAYS
+#define HTP_HA_LANE_ARRAYS 0
+#endif
+
 constexpr int MAXB = 8;       // body polygon vertices
 constexpr int MAXMOT = 16;    // motion primitives (King: 14, Pawn: 8)
 constexpr int MAXTRAJ = 64;   // poses per motion primitive (round(L/res) + 1)
@@ -337,10 +343,45 @@ struct Footprint {
     for (int k = 0; k < nb; ++k) {
       const int k1 = (k + 1) == nb ? 0 : k + 1;
       const double Ax = bx[k], Ay = by[k], Bx = bx[k1], By = by[k1];
+#if HTP_HA_LANE_ARRAYS
+      double lo[MAXJ], hi[MAXJ];
+      int n = 0;
+      for (int p = j0; p < j1; ++p) {
+        const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
+        const double* V = g.vert + 2 * o;
+        double l = 0.0, h = 1.0;
+        bool dead = false;
+        for (int i = 0; i < m; ++i) {
+          const int j = (i + 1) == m ? 0 : i + 1;
+          const double vx = V[2 * i], vy = V[2 * i + 1];
+          const double ex = V[2 * j] - vx, ey = V[2 * j + 1] - vy;
+          const double c0 = ex * (Ay - vy) - ey * (Ax - vx);
+          const double c1 = ex * (By - Ay) - ey * (Bx - Ax);
+          if (c1 > 0) { const double t = -c0 / c1; if (t > l) l = t; }
+          else if (c1 < 0) { const double t = -c0 / c1; if (t < h) h = t; }
+          else if (c0 < 0) dead = true;
+        }
+        if (!dead && l <= h) { lo[n] = l; hi[n] = h; ++n; }
+      }
+      // == sorted sweep "no gap, reach >= 1" (intervals lie in [0, 1])
+      double reach = 0.0;
+      bool grew = true;
+      while (grew) {
+        grew = false;
+        for (int i = 0; i < n; ++i) {
+          if (lo[i] <= reach) {
+            if (hi[i] > reach) reach = hi[i];
+            lo[i] = 2.0;  // consumed
+            grew = true;
+          }
+        }
+      }
+#else
       double reach = 0.0;
       for (int pass = 0; pass <= j1 - j0 && reach < 1.0; ++pass) {
-        bool grew = false;
-        for (int p = j0; p < j1; ++p) {
+        // another pass can only help if this one grew the reach AND left an interval starting beyond it
+        bool grew = false, skipped = false;
+        for (int p = j0; p < j1 && reach < 1.0; ++p) {
           const int o = g.poly_off[p], m = g.poly_off[p + 1] - o;
           const double* V = g.vert + 2 * o;
           double l = 0.0, h = 1.0;
@@ -355,10 +396,14 @@ struct Footprint {
             else if (c1 < 0) { const double t = -c0 / c1; if (t < h) h = t; }
             else if (c0 < 0) dead = true;
           }
-          if (!dead && l <= h && l <= reach && h > reach) { reach = h; grew = true; }
+          if (!dead && l <= h) {
+            if (l > reach) skipped = true;
+            else if (h > reach) { reach = h; grew = true; }
+          }
         }
-        if (!grew) break;
+        if (!grew || !skipped) break;
       }
+#endif
       if (!(reach >= 1.0)) return false;
     }
     return true;
