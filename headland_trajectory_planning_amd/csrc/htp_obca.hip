@@ -33,6 +33,23 @@ constexpr int LDS_D = LDS_WAVE_DOUBLES;  // scratch + filter + Riccati stage rin
 #define HTP_WAVES_PER_EU 1
 #endif
 
+// The solver's wave context (wave_ctx.h): DevWaveR (1) keeps the lane index and the LDS bases out of memory;
+// DevWave (0) holds them as fields (round 5)
+#ifndef HTP_CTX_REG
+#define HTP_CTX_REG 0
+#endif
+#if HTP_CTX_REG
+__shared__ double g_solver_lds[LDS_D];
+__shared__ int g_solver_ilds[2 * NBMAX];
+struct SolverLds {
+  __device__ __forceinline__ static DevWave::ld* d() { return (DevWave::ld*)g_solver_lds; }
+  __device__ __forceinline__ static DevWave::li* i() { return (DevWave::li*)g_solver_ilds; }
+};
+using SolverWave = DevWaveR<SolverLds>;
+#else
+using SolverWave = DevWave;
+#endif
+
 // Residency cap (experiment knob): HTP_WG_LDS_BYTES = LDS bytes claimed per problem
 // (workgroup), so at most floor(160 KB / that) solver waves share one CU.  The
 // kernel never touches the padding.  Unset or 0: no cap (4 waves per CU).
@@ -116,18 +133,24 @@ __global__ __launch_bounds__(64, HTP_WAVES_PER_EU) void obca_solve_kernel(const 
                                                         double* __restrict__ ws_all, int64_t ws_stride,
                                                         Result* __restrict__ res, double* __restrict__ xout,
                                                         WorkSrc src, OutView ov) {
+#if !HTP_CTX_REG
   __shared__ double lds_[LDS_D];
   __shared__ int ilds_[2 * NBMAX];
   DevWave::ld* lds = (DevWave::ld*)lds_;
   DevWave::li* ilds = (DevWave::li*)ilds_;
+#endif
   using CS = DevWave::cst<Shape>;
   CS* sh = (CS*)shp;
   double* ws = ws_all + (int64_t)blockIdx.x * ws_stride;
   long long t, p;
   while (claim(src, t, p)) {
-    DevWave c{(int)threadIdx.x, lds, ilds};
+#if HTP_CTX_REG
+    SolverWave c{};
+#else
+    SolverWave c{(int)threadIdx.x, lds, ilds};
+#endif
     ProblemIn in = problem_view(b, sh->D, p);
-    ObcaSolver<DevWave, EN, EM, FORM> S(c, sh->D, sh->L, sh->o, in, ws);
+    ObcaSolver<SolverWave, EN, EM, FORM> S(c, sh->D, sh->L, sh->o, in, ws);
     Result r{};
     S.run(r);
     if (threadIdx.x == 0) {

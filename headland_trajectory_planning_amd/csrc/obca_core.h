@@ -83,6 +83,31 @@ HTP_HD inline void sincos(double x, double& s, double& c) {
 // (0, the round-3 kernel) -- bit-identical results, fewer cycles in inertia-correction trials
 // Riccati factor: stage records staged through LDS HTP_FAC_SB stages at a time (0: one stage of register prefetch,
 // the round-4 kernel; bit-identical either way)
+// The Newton step's Riccati backward solve pass run inside the Riccati factor (1; exact dynamics only): the
+// backward recursion of the solve needs P_{i+1}, F_i and K_i, which the factor has at stage i, so its MFMAs
+// ride along with the factor's chain instead of a second pass over the stage records.  Same operands and the
+// same operation order as riccati_solve_mfma_t's backward pass: bit-identical.  0: a separate pass (round 5).
+// Round 6 A/B (config D 4 096, profiles/r06r_ab_D.txt): 3.45 M -> 3.36 M wave-cycles per problem-iteration.
+#ifndef HTP_BWD_FUSE
+#define HTP_BWD_FUSE 1
+#endif
+// Stage-chain loops with their invariants (workspace bases, sizes, the lane index, the relaxation flag) held in
+// locals set before the loop (1), or re-read inside it (0, round 5).  The solver object's address escapes into
+// the out-of-line phases, so after every wavefront fence each such read went back to memory through a pointer
+// chain -- and on gfx950 a load waits for every earlier store (one in-order vmcnt counter), so a re-read right
+// after a stage's stores cost the stores' full completion latency.  Values unchanged.
+#ifndef HTP_HOIST
+#define HTP_HOIST 1
+#endif
+// Riccati forward solve pass: Rt_i^-1 rt_i for a ring block's stages solved up front, one lane per stage (1), or
+// on the chain in each stage (0, round 5)
+#ifndef HTP_KV_HOIST
+#define HTP_KV_HOIST 1
+#endif
+// Riccati factor record loads without per-lane branches (1) or as conditional loads (0, round 5)
+#ifndef HTP_FILL_SEL
+#define HTP_FILL_SEL 1
+#endif
 #ifndef HTP_FAC_SB
 #define HTP_FAC_SB 4
 #endif
@@ -121,6 +146,14 @@ HTP_HD inline void sincos(double x, double& s, double& c) {
 // The barrier function (a log per bounded variable and slack, 8 loads per lane in flight) is evaluated at the
 // current point and at each line-search trial point from three sites; one out-of-line copy instead of three
 // inlined ones removes a sixth of the kernel's instructions (tools/code_size.py).
+// Cold IPM phases (watchdog, soft restoration, restoration entry / exit, pivoted local blocks on the serial
+// path): out of line (the default) or force-inlined (HTP_COLD_INLINE, experiments).  Out of line, the solver
+// object's address escapes into them.
+#ifdef HTP_COLD_INLINE
+#define HTP_COLD HTP_FI
+#else
+#define HTP_COLD __attribute__((noinline))
+#endif
 #ifndef HTP_BARRIER_INLINE
 #define HTP_BARRIER_ATTR __attribute__((noinline))
 #else
@@ -962,7 +995,9 @@ constexpr int RING_DOUBLES = (RING_SB + 1) * RS_L;
 #endif
 constexpr int PIV_LDS_PER_LANE = HTP_PIV_LDS ? 55 : 0;
 constexpr int LDS_WAVE_DOUBLES = RING_OFF + (RING_DOUBLES > 64 * PIV_LDS_PER_LANE ? RING_DOUBLES : 64 * PIV_LDS_PER_LANE);
-static_assert(HTP_FAC_SB >= 0 && RING_OFF + HTP_FAC_SB * 6 * 64 <= LDS_WAVE_DOUBLES, "factor staging exceeds the ring");
+constexpr int FAC_W_FB = 11;   // factor staging doubles per stage with the fused backward solve (HTP_BWD_FUSE)
+static_assert(HTP_FAC_SB >= 0 && RING_OFF + HTP_FAC_SB * (HTP_BWD_FUSE ? FAC_W_FB : 6) * 64 <= LDS_WAVE_DOUBLES,
+              "factor staging exceeds the ring");
 
 // ---------------------------------------------------------------------------
 template <class Ctx, int EN_ = 4, int EM_ = 4, int FORM_ = 0>
@@ -995,6 +1030,9 @@ struct ObcaSolver {
   // HTP_FUSE_RHS: the Newton step's local right-hand-side sweep runs inside the factor sweep (the blocks are
   // built and factored there already); kkt_solve then skips it.  The same per-block arithmetic: bit-identical.
   bool fuse_rhs = false;
+  // HTP_BWD_FUSE: the last factorization also ran the Newton right-hand side's Riccati backward pass (V and the
+  // backward half of X are in the workspace); the next fused-rhs kkt_solve starts at the forward pass
+  bool bwd_ready = false;
   // restoration phase (oracle/ipm.py RestoProblem): the iterate is [x, R] with R = [n_c | p_c | n_d | p_d] >= 0,
   // constraints c(x) + n_c - p_c = 0, d(x) + n_d - p_d - s = 0, objective rho sum R + eta/2 |D_R (x - x_R)|^2
   bool rs = false;
@@ -1058,6 +1096,24 @@ struct ObcaSolver {
 
   HTP_HD HTP_FI gd* A(int64_t off) const { return (gd*)(ws + off); }
   HTP_HD HTP_FI static const gd* gp(const double* p) { return (const gd*)p; }
+  // a wave-uniform pointer as the compiler's uniform value (scalar registers on the device)
+  template <class T>
+  HTP_HD HTP_FI static T* uptr(T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (T*)(((unsigned long long)hi << 32) | lo);
+#else
+    return p;
+#endif
+  }
+  // HTP_HOIST: what ring_fill reads besides the stage records
+  struct RingSrc { const gd* LD; const gd* fac; int N, nb, lane; bool relax; };
+  HTP_HD HTP_FI RingSrc ring_src() const {
+    return RingSrc{uptr((const gd*)A(L.LD)), uptr((const gd*)A(L.fac)), c.uniform_i(D.N), c.uniform_i(D.nb), (int)c.lane,
+                   c.uniform_i(ric_relax ? 1 : 0) != 0};
+  }
   HTP_HD HTP_FI double par(int k) const { return gp(in.par)[k]; }
   HTP_HD HTP_FI double tauv(const gd* x, int i) const { return D.topt ? x[D.oTAU + i] : 1.0; }
   // Upper bounds that exist (HTP_UB_SKIP): optimizer.py's multipliers mu, lambda ([oMU, oTAU), :292-354) have a
@@ -1350,6 +1406,24 @@ struct ObcaSolver {
     const gd* scE = A(L.scE);
     const gd* scI = A(L.scI);
     for (int i = c.lane; i < N; i += c.width) {
+#if HTP_HOIST
+      // every load of the stage before its first store (a load issued after a store waits for it)
+      double e0[NS], x0[NS], t0[NS];
+      if (i == 0)
+        for (int k = 0; k < NS; ++k) { e0[k] = scE[k]; x0[k] = x[k]; t0[k] = gp(in.traj)[k]; }
+      if (i < N - 1) {
+        double w[8], F[5], ek[NS], xk[NS];
+        stage_w(x, i, w);
+        for (int k = 0; k < NS; ++k) {
+          ek[k] = scE[D.eDyn + NS * i + k];
+          xk[k] = x[NS * (i + 1) + k];
+        }
+        dynF(w, F);
+        if (i == 0)
+          for (int k = 0; k < NS; ++k) cc[k] = e0[k] * (x0[k] - t0[k]);
+        for (int k = 0; k < NS; ++k) cc[D.eDyn + NS * i + k] = ek[k] * (xk[k] - F[k]);
+      } else {
+#else
       if (i == 0)
         for (int k = 0; k < NS; ++k) cc[k] = scE[k] * (x[k] - gp(in.traj)[k]);
       if (i < N - 1) {
@@ -1361,11 +1435,26 @@ struct ObcaSolver {
           cc[r] = scE[r] * (x[NS * (i + 1) + k] - F[k]);
         }
       } else {
+#endif
+#if HTP_HOIST
+        double ek[NS], xk[NS], tk[NS], sk[NS];
+        for (int k = 0; k < NS; ++k) {
+          ek[k] = scE[D.eTerm + k];
+          xk[k] = x[NS * i + k];
+          tk[k] = gp(in.traj)[NS * i + k];
+          sk[k] = PT ? 0.0 : x[D.oS + k];
+        }
+        for (int k = 0; k < NS; ++k) {
+          if constexpr (PT) cc[D.eTerm + k] = ek[k] * (xk[k] - tk[k]);
+          else cc[D.eTerm + k] = ek[k] * (xk[k] - tk[k] + sk[k]);
+        }
+#else
         for (int k = 0; k < NS; ++k) {
           const int r = D.eTerm + k;
           if constexpr (PT) cc[r] = scE[r] * (x[NS * i + k] - gp(in.traj)[NS * i + k]);
           else cc[r] = scE[r] * (x[NS * i + k] - gp(in.traj)[NS * i + k] + x[D.oS + k]);
         }
+#endif
       }
     }
     if constexpr (PT) {
@@ -1388,12 +1477,21 @@ struct ObcaSolver {
     }
     for (int p = c.lane; p < D.P; p += c.width) {
       double v[4];
-      pair_cons(x, p, v);
       const int re = D.ePair + 2 * p;
+#if HTP_HOIST
+      const double sa = scE[re], sb = scE[re + 1], s1 = scI[2 * p], s3 = scI[2 * p + 1];
+      pair_cons(x, p, v);
+      cc[re] = sa * v[1];
+      cc[re + 1] = sb * v[2];
+      dd[2 * p] = s1 * v[0];
+      dd[2 * p + 1] = s3 * v[3];
+#else
+      pair_cons(x, p, v);
       cc[re] = scE[re] * v[1];
       cc[re + 1] = scE[re + 1] * v[2];
       dd[2 * p] = scI[2 * p] * v[0];
       dd[2 * p + 1] = scI[2 * p + 1] * v[3];
+#endif
     }
     c.sync();
   }
@@ -1894,7 +1992,7 @@ struct ObcaSolver {
   // Local block p with Bunch-Kaufman interchanges (rare): rebuild, factor,
   // solve the nrhs right-hand sides V[k*NL ...] in place.
   template <int EN, int EM>
-  __attribute__((noinline)) HTP_HD void local_pivoted(int p, bool ls, double dw, double dc, double* V, int nrhs,
+  HTP_COLD HTP_HD void local_pivoted(int p, bool ls, double dw, double dc, double* V, int nrhs,
                                                       int* inertia) const {
     constexpr int NL = LocalBlock<EN, EM>::NL;
     constexpr int NPK = LocalBlock<EN, EM>::NPK;
@@ -2150,6 +2248,18 @@ struct ObcaSolver {
               for (int r = 0; r < NL; ++r) acc += W[row][r] * (W[col][r] * id[r]);
               S[sidx(row, col)] = acc;
             }
+#if HTP_HOIST
+          // the fused right-hand side's loads before the block's first store (a load waits for earlier stores)
+          if (fuse_rhs) {   // the Newton step's right-hand side (kkt_solve's local_rhs_sweep, fused)
+            double v[NL], q3;
+            local_rhs_vec<EN, EM>(p, B, A(L.xt), A(L.rs), A(L.rc), A(L.rd), v, q3);
+            B.solve(v);
+            for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
+            local_rhs_out<EN, EM>(p, B, v, q3, A(L.pairR));
+          } else {
+            for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
+          }
+#else
           for (int k = 0; k < 6; ++k) PS[6 * p + k] = B.Hpp[k] - S[k];
           if (fuse_rhs) {   // the Newton step's right-hand side (kkt_solve's local_rhs_sweep, fused)
             double v[NL], q3;
@@ -2157,6 +2267,7 @@ struct ObcaSolver {
             B.solve(v);
             local_rhs_out<EN, EM>(p, B, v, q3, A(L.pairR));
           }
+#endif
 #ifdef HTP_LPROF
           const long long ls0 = c.clock();
 #endif
@@ -2512,7 +2623,7 @@ struct ObcaSolver {
     }
   }
 
-  __attribute__((noinline)) HTP_HD void local_pivoted_pt(int p, bool ls, double dw, double dc, double* V, int nrhs,
+  HTP_COLD HTP_HD void local_pivoted_pt(int p, bool ls, double dw, double dc, double* V, int nrhs,
                                                          int* inertia) const {
     PtGeom G;
     pt_geom(A(L.x), p, G);
@@ -3440,12 +3551,20 @@ struct ObcaSolver {
   // The stage chain's v-block width nv = nw - 5 (2: u; 3: u and tau with time-optimal scaling) as a template
   // argument: every per-lane index test and the 3 x 3 Cholesky unroll at compile time (28 % fewer cycles per
   // factor stage, tools/micro/ric_micro.hip); the arithmetic is unchanged.
-  HTP_HD HTP_FI int riccati_factor_mfma(double dc) {
-    if constexpr (PT) return riccati_factor_mfma_t<2>(dc);
-    else return D.nw == NS + 3 ? riccati_factor_mfma_t<3>(dc) : riccati_factor_mfma_t<2>(dc);
+  HTP_HD HTP_FI int riccati_factor_mfma(double dc, bool fb = false) {
+    if constexpr (PT) return riccati_factor_mfma_t<2, false>(dc);
+    else {
+#if HTP_BWD_FUSE
+      if (fb && !ric_relax) return D.nw == NS + 3 ? riccati_factor_mfma_t<3, true>(dc) : riccati_factor_mfma_t<2, true>(dc);
+#endif
+      return D.nw == NS + 3 ? riccati_factor_mfma_t<3, false>(dc) : riccati_factor_mfma_t<2, false>(dc);
+    }
   }
-  template <int NV>
+  // FB: also the backward pass of riccati_solve_mfma_t for the stage right-hand side V already in the workspace
+  // (exact dynamics): p_i, rt_i into X exactly as that pass writes them.
+  template <int NV, bool FB>
   HTP_HD HTP_FI int riccati_factor_mfma_t(double dc) {
+    static_assert(!FB || HTP_FAC_SB > 0, "the fused backward pass reads its records from the factor staging");
     constexpr int nv = NV, nz = NS + nv;
     const int N = D.N, nb = D.nb;
     const int64_t nb2 = (int64_t)nb * nb;
@@ -3468,6 +3587,23 @@ struct ObcaSolver {
     const gd* Kst = A(L.Kst);
     const gd* Off = A(L.Off);
     const gd* LDa = A(L.LD);
+#if HTP_FILL_SEL
+    // every record load issued unconditionally from an in-range address, then selected: a load under a per-lane
+    // branch let the compiler's wait-count pass put a vmcnt(0) wait between the batch's loads
+    auto ld_h = [&](int i, double* h) {
+      for (int r = 0; r < 4; ++r) {
+        const gd* src = hk[r] == 2 ? Off : Kst;
+        const double t = src[(int64_t)i * nb2 + ho[r]];
+        h[r] = (hk[r] == 1 || (hk[r] == 2 && i >= 1)) ? t : 0.0;
+      }
+    };
+    auto ld_f = [&](int i, double* f) {
+      for (int sgm = 0; sgm < 2; ++sgm) {
+        const double t = LDa[(int64_t)i * nb2 + (fs[sgm].kind == 3 ? fs[sgm].off : 0)];
+        f[sgm] = fs[sgm].kind == 3 ? t : (fs[sgm].kind == 4 ? 1.0 : 0.0);
+      }
+    };
+#else
     auto ld_h = [&](int i, double* h) {
       for (int r = 0; r < 4; ++r) {
         double v = 0.0;
@@ -3479,6 +3615,7 @@ struct ObcaSolver {
     auto ld_f = [&](int i, double* f) {
       for (int sgm = 0; sgm < 2; ++sgm) f[sgm] = f_get(fs[sgm], LDa + (int64_t)i * nb2);
     };
+#endif
     // P_{N-1} = [[H_xx, 0], [0, 0]]
     dbl4 Pc;
     {
@@ -3488,9 +3625,35 @@ struct ObcaSolver {
         const double v = (row < NS && col < NS) ? Kst[(int64_t)(N - 1) * nb2 + (NS + row) * nb + NS + col] : 0.0;
         Pc[r] = v;
         if (row < 8 && col < 8) Ps[row * 8 + col] = v;
+        if (FB && row < 8 && col < 8) Pb[row * 8 + col] = v;   // P_{N-1} as the solve's first stage reads it
       }
     }
     int bad = 0;
+    const gd* Vg = A(L.V);
+    gd* Xg = A(L.X);
+#if HTP_HOIST
+    gd* const LDw = uptr(A(L.LD));
+    const int ln = c.lane;
+    const bool relax_f = c.uniform_i(ric_relax ? 1 : 0) != 0;
+#else
+    gd* const LDw = nullptr;
+    const int ln = 0;
+    const bool relax_f = false;
+#endif
+    const bool c0 = col == 0;
+    dbl4 pv = {0.0, 0.0, 0.0, 0.0};                  // the solve's p_{i+1} (riccati_solve_mfma_t, backward)
+    if constexpr (FB) {
+      for (int r = 0; r < 2; ++r) {
+        const int row = rg + 4 * r;
+        pv[r] = (c0 && row < NS) ? Vg[(int64_t)(N - 1) * nb + NS + row] : 0.0;
+      }
+      gd* Xl = Xg + (int64_t)(N - 1) * nb;
+      for (int r = 0; r < 2; ++r) {
+        const int row = rg + 4 * r;
+        if (c0 && row < 8) Xl[row] = pv[r];
+      }
+      c.sync();
+    }
     // relaxed rows: P_i goes through LDS (Pb) into relax_P and back into the C-layout registers
     auto relax_regs = [&](int i) {
       for (int r = 0; r < 2; ++r) {
@@ -3513,32 +3676,63 @@ struct ObcaSolver {
     // stage (a stage's work is shorter than a load's latency under load, and every load also waits for the
     // previous stages' P / K / chol stores, which the in-order vmcnt counter places before it).  Same values.
     ld* fring = c.lds + RING_OFF;
+    constexpr int FW = FB ? FAC_W_FB : 6;   // per stage: H (4), F (2)[, e_{i+1} (2), [q_i; r_i] (3)]
+    // the solve's stage-i record (riccati_solve_mfma_t ld_b): e_{i+1} = V_{i+1} / sc, [q_i; r_i] from V_i
+    auto ld_s = [&](int i, double* e) {
+      for (int sgm = 0; sgm < 2; ++sgm) {
+        const int row = rg + 4 * sgm;
+        const bool on = c0 && row < NS;
+        const int rr = on ? row : 0;
+        const double a = Vg[(int64_t)(i + 1) * nb + rr], b = LDa[(int64_t)(i + 1) * nb2 + SOFF + rr];
+        e[sgm] = on ? a * b : 0.0;
+      }
+      for (int r = 0; r < 3; ++r) {
+        const int row = rg + 4 * r;
+        const bool on1 = c0 && row < NS, on2 = c0 && row >= V0 && row < V0 + nv;
+        const int off = on1 ? NS + row : (on2 ? NS + NS + (row - V0) : 0);
+        const double t = Vg[(int64_t)i * nb + off];
+        e[2 + r] = (on1 || on2) ? t : 0.0;
+      }
+    };
     auto fac_fill = [&](int hi) {   // stages hi, hi - 1, ..., hi - HTP_FAC_SB + 1 (those >= 0)
-      double v[HTP_FAC_SB][6];
+      double v[HTP_FAC_SB][FW];
 #pragma unroll
       for (int sb = 0; sb < HTP_FAC_SB; ++sb) {
         const int st = hi - sb >= 0 ? hi - sb : 0;
         ld_h(st, v[sb]);
         ld_f(st, v[sb] + 4);
+        if constexpr (FB) ld_s(st, v[sb] + 6);
       }
 #pragma unroll
       for (int sb = 0; sb < HTP_FAC_SB; ++sb)
 #pragma unroll
-        for (int k = 0; k < 6; ++k) fring[(sb * 6 + k) * 64 + c.lane] = v[sb][k];
+        for (int k = 0; k < FW; ++k) fring[(sb * FW + k) * 64 + (HTP_HOIST ? ln : (int)c.lane)] = v[sb][k];
     };
     for (int i = N - 2; i >= 0; --i) {
       HTP_PROF0();
       const int sb = (N - 2 - i) % HTP_FAC_SB;
       if (sb == 0) fac_fill(i);
-      for (int r = 0; r < 4; ++r) hcur[r] = fring[(sb * 6 + r) * 64 + c.lane];
-      fcur[0] = fring[(sb * 6 + 4) * 64 + c.lane];
-      fcur[1] = fring[(sb * 6 + 5) * 64 + c.lane];
+      const int lnc = HTP_HOIST ? ln : (int)c.lane;
+      for (int r = 0; r < 4; ++r) hcur[r] = fring[(sb * FW + r) * 64 + lnc];
+      fcur[0] = fring[(sb * FW + 4) * 64 + lnc];
+      fcur[1] = fring[(sb * FW + 5) * 64 + lnc];
+      // the solve's -P_{i+1} (A operand, from the unsymmetrised P_{i+1} the factor stored: Pb still holds it)
+      double smp[2], sre[5];
+      if constexpr (FB) {
+        for (int sgm = 0; sgm < 2; ++sgm) {
+          const int k = rg + 4 * sgm;
+          smp[sgm] = -((col < nz && k < nz) ? (double)Pb[col * 8 + k] : 0.0);
+        }
+        for (int k = 0; k < 5; ++k) sre[k] = fring[(sb * FW + 6 + k) * 64 + lnc];
+      }
 #else
     double hnxt[4], fnxt[2];
     if (N >= 2) { ld_h(N - 2, hcur); ld_f(N - 2, fcur); }
     for (int i = N - 2; i >= 0; --i) {
       HTP_PROF0();
       if (i > 0) { ld_h(i - 1, hnxt); ld_f(i - 1, fnxt); }  // next stage's record, in flight during this one
+      const int lnc = HTP_HOIST ? ln : (int)c.lane;
+      double smp[2], sre[5];
 #endif
       dbl4 Y = {0.0, 0.0, 0.0, 0.0};
       Y = Ctx::mfma16(Pc[0], fcur[0], Y);
@@ -3549,6 +3743,14 @@ struct ObcaSolver {
       if (rg < nv) Mv[rg * 16 + col] = M[2];  // rows V0 + rg (register 2)
       c.sync();
       HTP_PROF(1);
+      dbl4 sg = {0.0, 0.0, 0.0, 0.0};
+      if constexpr (FB) {                            // w = p - P e;  g = [q; r] + F' w
+        dbl4 w = Ctx::mfma16(smp[0], sre[0], pv);
+        w = Ctx::mfma16(smp[1], sre[1], w);
+        sg = dbl4{sre[2], sre[3], sre[4], 0.0};
+        sg = Ctx::mfma16(fcur[0], w[0], sg);
+        sg = Ctx::mfma16(fcur[1], w[1], sg);
+      }
       double Rl[9], Lc[9];
       for (int k = 0; k < 9; ++k) Rl[k] = (k / 3 < nv && k % 3 < nv) ? Mv[(k / 3) * 16 + V0 + k % 3] : 0.0;
       const bool pd = chol3(Rl, nv, Lc);
@@ -3561,21 +3763,31 @@ struct ObcaSolver {
       const double kB = (rg < nv && col < nz) ? -stc[rg] : 0.0;  // K[rg][col] as the B operand
       HTP_PROF(3);
       const dbl4 Pn = Ctx::mfma16(stA, kB, M);
-      gd* Ps = A(L.LD) + (int64_t)i * nb2;
+      if constexpr (FB) {                            // p = g_z + K' rt;  X_i = [p_i; rt_i]
+        const double kt = (rg < nv && col < nz) ? kB : 0.0;
+        pv = Ctx::mfma16(kt, sg[2], sg);
+        gd* Xi = Xg + (int64_t)i * nb;
+        for (int r = 0; r < 2; ++r) {
+          const int row = rg + 4 * r;
+          if (c0 && row < nz) Xi[row] = pv[r];
+        }
+        if (c0 && rg < nv) Xi[nz + rg] = sg[2];
+      }
+      gd* Ps = (HTP_HOIST ? LDw : A(L.LD)) + (int64_t)i * nb2;
       for (int r = 0; r < 2; ++r) {
         const int row = rg + 4 * r;
         const double v = (row < nz && col < nz) ? Pn[r] : 0.0;
         if (col < 8) { Pb[row * 8 + col] = v; Ps[row * 8 + col] = v; }
       }
       if (rg < 3 && col < 8) Ps[64 + rg * 8 + col] = (rg < nv && col < nz) ? kB : 0.0;
-      if (c.lane < 9) Ps[88 + c.lane] = Lc[c.lane];
+      if (lnc < 9) Ps[88 + lnc] = Lc[lnc];
       c.sync();
       for (int r = 0; r < 4; ++r) {  // P_i = (Pn + Pn') / 2, zero outside nz x nz
         const int row = rg + 4 * r;
         Pc[r] = (r < 2 && row < nz && col < nz) ? 0.5 * (Pb[row * 8 + col] + Pb[col * 8 + row]) : 0.0;
       }
       c.sync();
-      if (ric_relax) relax_regs(i);
+      if (HTP_HOIST ? relax_f : ric_relax) relax_regs(i);
 #if HTP_FAC_SB == 0
       for (int r = 0; r < 4; ++r) hcur[r] = hnxt[r];
       fcur[0] = fnxt[0];
@@ -3735,9 +3947,13 @@ struct ObcaSolver {
   // the MFMA operands of stage i are then gathered from LDS one stage ahead (values unchanged:
   // bit-identical to gathering them from HBM).
   // stages [lo, lo + cnt) of LD / V / X into the ring (cnt <= RING_SB + 1); stages >= N skipped
-  HTP_HD HTP_FI void ring_fill(ld* ring, int lo, int cnt, const gd* V, const gd* X) {
-    const int N = D.N, nb = D.nb;
+  HTP_HD HTP_FI void ring_fill(ld* ring, int lo, int cnt, const gd* V, const gd* X, const RingSrc* hs = nullptr) {
+    const int N = hs ? hs->N : D.N, nb = hs ? hs->nb : D.nb;
     const int64_t nb2 = (int64_t)nb * nb;
+    const int lane_ = hs ? hs->lane : (int)c.lane;
+    const bool relax_ = hs ? hs->relax : ric_relax;
+    const gd* LDs = hs ? hs->LD : A(L.LD);
+    const gd* FAs = hs ? hs->fac : A(L.fac);
 #if HTP_RING_FILL_LANE
     // Lane l copies elements k = l + 64 j (j < 4) of every stage record; where element k comes from (LD slot,
     // V_i, X_i or the T / Q records in fac) does not depend on the stage, so the four sources are resolved once
@@ -3748,11 +3964,11 @@ struct ObcaSolver {
     bool ok[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      const int k = c.lane + 64 * j;
-      if (k < RS_SLOT) { src[j] = A(L.LD) + k; strd[j] = nb2; ok[j] = true; }
+      const int k = lane_ + 64 * j;
+      if (k < RS_SLOT) { src[j] = LDs + k; strd[j] = nb2; ok[j] = true; }
       else if (k < RS_X) { src[j] = V + (k - RS_V); strd[j] = nb; ok[j] = k - RS_V < nb; }
       else if (k < RS_T) { src[j] = X + (k - RS_X); strd[j] = nb; ok[j] = k - RS_X < nb; }
-      else { src[j] = A(L.fac) + (k < RS_L ? k - RS_T : 0); strd[j] = nb2; ok[j] = k < RS_L && ric_relax; }
+      else { src[j] = FAs + (k < RS_L ? k - RS_T : 0); strd[j] = nb2; ok[j] = k < RS_L && relax_; }
     }
     double v[RING_SB + 1][J];
 #pragma unroll
@@ -3767,7 +3983,7 @@ struct ObcaSolver {
     for (int sb = 0; sb <= RING_SB; ++sb)
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        const int k = c.lane + 64 * j;
+        const int k = lane_ + 64 * j;
         if (sb < cnt && k < RS_L) ring[sb * RS_L + k] = v[sb][j];
       }
 #else
@@ -3795,13 +4011,14 @@ struct ObcaSolver {
 #endif
   }
 
-  HTP_HD HTP_FI void riccati_solve_mfma(const gd* V, gd* X) {
+  HTP_HD HTP_FI void riccati_solve_mfma(const gd* V, gd* X, bool skip_bwd = false) {
     if constexpr (PT) riccati_solve_mfma_t<2>(V, X);
-    else if (D.nw == NS + 3) riccati_solve_mfma_t<3>(V, X);
-    else riccati_solve_mfma_t<2>(V, X);
+    else if (D.nw == NS + 3) riccati_solve_mfma_t<3>(V, X, skip_bwd);
+    else riccati_solve_mfma_t<2>(V, X, skip_bwd);
   }
+  // skip_bwd: the backward pass already ran inside the factorization (HTP_BWD_FUSE); X holds p_i, rt_i
   template <int NV>
-  HTP_HD HTP_FI void riccati_solve_mfma_t(const gd* V, gd* X) {
+  HTP_HD HTP_FI void riccati_solve_mfma_t(const gd* V, gd* X, bool skip_bwd = false) {
 #if defined(HTP_KKT_PROF) && HTP_KKT_PROF == 2
     long long kt_ric = c.clock();
 #endif
@@ -3830,7 +4047,7 @@ struct ObcaSolver {
       const int row = rg + 4 * r;
       pv[r] = (c0 && row < NS) ? V[(int64_t)(N - 1) * nb + NS + row] : 0.0;
     }
-    {
+    if (!skip_bwd) {
       gd* Xl = X + (int64_t)(N - 1) * nb;
       for (int r = 0; r < 2; ++r) {
         const int row = rg + 4 * r;
@@ -3846,6 +4063,8 @@ struct ObcaSolver {
     };
     const bool rlx = ric_relax;
     const dbl4 z4 = {0.0, 0.0, 0.0, 0.0};
+    const RingSrc hsrc = ring_src();
+    (void)hsrc;
     struct BRec { double mp[2], ft[2], kt, qr[3], e[2], ta[2], qa[2]; };
     auto ld_b = [&](int i, BRec& R) {
       const ld* slot = rs(i);
@@ -3868,11 +4087,11 @@ struct ObcaSolver {
       }
     };
     BRec bc, bn;
-    for (int hi = N - 2; hi >= 0; hi -= RING_SB) {
+    for (int hi = skip_bwd ? -1 : N - 2; hi >= 0; hi -= RING_SB) {
       lo = hi - RING_SB + 1 > 0 ? hi - RING_SB + 1 : 0;
       c.sync();                                       // the previous block's LDS reads are done
       HTP_SPROF0();
-      ring_fill(ring, lo, hi - lo + 2, V, X);         // stages lo .. hi + 1
+      ring_fill(ring, lo, hi - lo + 2, V, X, HTP_HOIST ? &hsrc : nullptr);         // stages lo .. hi + 1
       c.sync();
       ld_b(hi, bc);
       HTP_SPROF(0);
@@ -3935,15 +4154,31 @@ struct ObcaSolver {
       }
       for (int sgm = 0; sgm < 3; ++sgm) R.fa[sgm] = last ? 0.0 : f_at(fA[sgm], slot);
       for (int a = 0; a < 3; ++a) R.rt[a] = (!last && a < nv) ? (double)slot[RS_X + nz + a] : 0.0;
+#if !HTP_KV_HOIST
       for (int k = 0; k < 9; ++k) R.lc[k] = last ? 0.0 : (double)slot[88 + k];
+#endif
     };
     FRec fc, fn;
     for (lo = 0; lo < N; lo += RING_SB) {
       const int hi = lo + RING_SB - 1 < N - 1 ? lo + RING_SB - 1 : N - 1;
       c.sync();
       HTP_SPROF0();
-      ring_fill(ring, lo, hi - lo + 2, V, X);         // stages lo .. hi + 1 (X_i holds p_i, rt_i here)
+      ring_fill(ring, lo, hi - lo + 2, V, X, HTP_HOIST ? &hsrc : nullptr);   // stages lo .. hi + 1 (X_i: p_i, rt_i)
       c.sync();
+#if HTP_KV_HOIST
+      // Rt_i^-1 rt_i does not depend on the forward recursion: one lane per stage of the block solves it and
+      // leaves it in the stage's rt slot (the same chol3_solve on the same values), off the chain
+      if (hsrc.lane <= hi - lo && lo + hsrc.lane < N - 1) {
+        ld* sl = ring + hsrc.lane * RS_L;
+        double kv[3], lc[9];
+        for (int a = 0; a < 3; ++a) kv[a] = a < nv ? (double)sl[RS_X + nz + a] : 0.0;
+        for (int k = 0; k < 9; ++k) lc[k] = sl[88 + k];
+        chol3_solve(lc, nv, kv);
+        for (int a = 0; a < 3; ++a)
+          if (a < nv) sl[RS_X + nz + a] = kv[a];
+      }
+      c.sync();
+#endif
       ld_f(lo, fc);
       HTP_SPROF(2);
       for (int i = lo; i <= hi; ++i) {
@@ -3969,7 +4204,9 @@ struct ObcaSolver {
         }
         if (i < N - 1) {
           double kv[3] = {fc.rt[0], fc.rt[1], fc.rt[2]};
+#if !HTP_KV_HOIST
           chol3_solve(fc.lc, nv, kv);
+#endif
           dbl4 u = {zu[0], zu[1], (c0 && rg < nv) ? kv[rg] : 0.0, 0.0};  // u = [z; Rt^-1 rt + K z]
           u = Ctx::mfma16(fc.ka[0], zu[0], u);
           u = Ctx::mfma16(fc.ka[1], zu[1], u);
@@ -4271,9 +4508,9 @@ struct ObcaSolver {
   //   (S_T Sig S_T + E_T) y_T = s_T o (K^-1 r_Z)_x - r_T,   Sig = K^-1 [x_{N-1}, x_{N-1}],
   // then Z = K^-1 (r_Z - C' y_T).  Inertia (Sylvester, Schur on y_T): the 5 terminal negatives iff
   // S_T Sig S_T + E_T is positive definite.  Sig = five solves with unit right-hand sides at x_{N-1}.
-  HTP_HD HTP_FI void ric_solve(const gd* V, gd* X) {
+  HTP_HD HTP_FI void ric_solve(const gd* V, gd* X, bool skip_bwd = false) {
 #if defined(__HIPCC__) || defined(HTP_EMU_WAVE)
-    if constexpr (Ctx::kMfma) { riccati_solve_mfma(V, X); return; }
+    if constexpr (Ctx::kMfma) { riccati_solve_mfma(V, X, skip_bwd); return; }
 #endif
     riccati_solve(V, X);
   }
@@ -4343,6 +4580,7 @@ struct ObcaSolver {
     const int N = D.N, nb = D.nb;
     int neg = 0, zero = 0;
     long long t0 = c.clock();
+    bwd_ready = false;
     if (rs) compute_eR(ls, dw);
     local_factor_sweep<EN_, EM_>(ls, dw, dc, neg, zero);
     neg = c.isum(neg);
@@ -4380,7 +4618,18 @@ struct ObcaSolver {
       int bad;
       ric_relax = dc != 0.0 || rs;
 #if defined(__HIPCC__) || defined(HTP_EMU_WAVE)
-      if constexpr (Ctx::kMfma) bad = riccati_factor_mfma(dc);
+      if constexpr (Ctx::kMfma) {
+#if HTP_BWD_FUSE
+        // the Newton step's rhs is known here (fused local sweep: pairR is this trial's): build V and run the
+        // solve's backward pass with the factor
+        const bool fb = fuse_rhs && !PT && !ric_relax && !ls;
+        if (fb) { build_stage_rhs(ls, dw, dc, A(L.xt), A(L.rc)); c.sync(); }
+        bad = riccati_factor_mfma(dc, fb);
+        bwd_ready = fb && !bad;
+#else
+        bad = riccati_factor_mfma(dc);
+#endif
+      }
       else
 #endif
         bad = riccati_factor(dc);
@@ -4469,6 +4718,44 @@ struct ObcaSolver {
     c.sync();
   }
 
+  // stage right-hand side V (block order [y|x|u|tau]) of the KKT system from bx, bc and the local blocks' stage
+  // contributions (pairR); each stage's rhs is built in registers and stored once
+  HTP_HD HTP_FI void build_stage_rhs(bool ls, double dw, double dc, const gd* bx, const gd* bc) {
+    const int N = D.N, nb = D.nb;
+    const gd* PR = A(L.pairR);
+    const gd* scE = A(L.scE);
+    gd* V = A(L.V);
+    const int MK = blocks_per_stage();
+    for (int i = c.lane; i < N; i += c.width) {
+      gd* r = V + (int64_t)i * nb;
+      const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
+      double rv[NBMAX];
+      for (int k = 0; k < NS; ++k) rv[k] = bc[rowbase + k];
+      for (int k = 0; k < NS; ++k) rv[NS + k] = bx[NS * i + k];
+      for (int a = NS; a < NBMAX - NS; ++a) rv[NS + a] = 0.0;
+      if (i < N - 1) {
+        rv[NS + 5] = bx[D.oU + NC * i];
+        rv[NS + 6] = bx[D.oU + NC * i + 1];
+        if (D.topt) rv[NS + 7] = bx[D.oTAU + i];
+      } else {
+        if constexpr (!PT)
+          for (int k = 0; k < NS; ++k) {
+            const double st = scE[D.eTerm + k];
+            const double Hs = term_H(k, ls, dw), Et = term_E(k, ls, dw, dc);
+            rv[NS + k] -= st / Et * (st * bx[D.oS + k] / Hs - bc[D.eTerm + k]);
+          }
+      }
+      for (int q = 0; q < MK; ++q) {
+        const int p = blk(i, q);
+        rv[NS + 0] += PR[3 * p];
+        rv[NS + 1] += PR[3 * p + 1];
+        rv[NS + 3] += PR[3 * p + 2];
+      }
+      for (int a = 0; a < NBMAX; ++a)
+        if (a < nb) r[a] = rv[a];
+    }
+  }
+
   HTP_HD HTP_PHASE void kkt_solve(bool ls, double dw, double dc, const gd* bx, const gd* bs, const gd* bc,
                         const gd* bd, gd* ox, gd* os, gd* oc, gd* od, const gd* bR = nullptr, gd* oR = nullptr,
                         bool rhs_done = false) {
@@ -4502,39 +4789,15 @@ struct ObcaSolver {
 #if defined(HTP_KKT_PROF) && HTP_KKT_PROF == 2
     kprof[6] += 1;
 #endif
-    const gd* PR = A(L.pairR);
     const gd* scE = A(L.scE);
     gd* V = A(L.V);
-    const int MK = blocks_per_stage();
-    for (int i = c.lane; i < N; i += c.width) {
-      // the stage rhs is built in registers and stored once (no read-modify-write in HBM)
-      gd* r = V + (int64_t)i * nb;
-      const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
-      double rv[NBMAX];
-      for (int k = 0; k < NS; ++k) rv[k] = bc[rowbase + k];
-      for (int k = 0; k < NS; ++k) rv[NS + k] = bx[NS * i + k];
-      for (int a = NS; a < NBMAX - NS; ++a) rv[NS + a] = 0.0;
-      if (i < N - 1) {
-        rv[NS + 5] = bx[D.oU + NC * i];
-        rv[NS + 6] = bx[D.oU + NC * i + 1];
-        if (D.topt) rv[NS + 7] = bx[D.oTAU + i];
-      } else {
-        if constexpr (!PT)
-          for (int k = 0; k < NS; ++k) {
-            const double st = scE[D.eTerm + k];
-            const double Hs = term_H(k, ls, dw), Et = term_E(k, ls, dw, dc);
-            rv[NS + k] -= st / Et * (st * bx[D.oS + k] / Hs - bc[D.eTerm + k]);
-          }
-      }
-      for (int q = 0; q < MK; ++q) {
-        const int p = blk(i, q);
-        rv[NS + 0] += PR[3 * p];
-        rv[NS + 1] += PR[3 * p + 1];
-        rv[NS + 3] += PR[3 * p + 2];
-      }
-      for (int a = 0; a < NBMAX; ++a)
-        if (a < nb) r[a] = rv[a];
-    }
+#if HTP_BWD_FUSE
+    const bool bwd = rhs_done && bwd_ready;   // V and the backward pass came with the factorization
+#else
+    const bool bwd = false;
+#endif
+    bwd_ready = false;
+    if (!bwd) build_stage_rhs(ls, dw, dc, bx, bc);
     if constexpr (PT)
       for (int e = c.lane; e < nb; e += c.width) V[(int64_t)N * nb + e] = (e < NS) ? bc[D.eTerm + e] : 0.0;
     c.sync();
@@ -4544,7 +4807,7 @@ struct ObcaSolver {
     gd* X = A(L.X);
     if (use_ric) {
       if constexpr (PT) ric_solve_terminal(V, X);
-      else ric_solve(V, X);
+      else ric_solve(V, X, bwd);
     } else {
     // forward: V_i -= LD_i V_{i-1}
     for (int i = 1; i < D.nblk; ++i) {
@@ -4583,6 +4846,46 @@ struct ObcaSolver {
     }
     }
     // scatter stage solution
+#if HTP_HOIST
+    // every load of the stage before its first store (a load issued after a store waits for it)
+    for (int i = c.lane; i < N; i += c.width) {
+      const gd* xg = X + (int64_t)i * nb;
+      double xi[NBMAX];
+      for (int a = 0; a < NBMAX; ++a) xi[a] = xg[a < nb ? a : 0];
+      const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
+      if (i == N - 1) {
+        if constexpr (PT) {
+          double xt_[NS];
+          for (int k = 0; k < NS; ++k) xt_[k] = X[(int64_t)N * nb + k];
+          for (int k = 0; k < NS; ++k) oc[rowbase + k] = xi[k];
+          for (int k = 0; k < NS; ++k) ox[NS * i + k] = xi[NS + k];
+          for (int k = 0; k < NS; ++k) oc[D.eTerm + k] = xt_[k];
+        } else {
+          double yt[NS], xs[NS];
+          for (int k = 0; k < NS; ++k) {
+            const double st = scE[D.eTerm + k];
+            const double Hs = term_H(k, ls, dw), Et = term_E(k, ls, dw, dc);
+            const double bxs = bx[D.oS + k];
+            yt[k] = (st * xi[NS + k] + st * bxs / Hs - bc[D.eTerm + k]) / Et;
+            xs[k] = (bxs - st * yt[k]) / Hs;
+          }
+          for (int k = 0; k < NS; ++k) oc[rowbase + k] = xi[k];
+          for (int k = 0; k < NS; ++k) ox[NS * i + k] = xi[NS + k];
+          for (int k = 0; k < NS; ++k) {
+            oc[D.eTerm + k] = yt[k];
+            ox[D.oS + k] = xs[k];
+          }
+        }
+      } else {
+        for (int k = 0; k < NS; ++k) oc[rowbase + k] = xi[k];
+        for (int k = 0; k < NS; ++k) ox[NS * i + k] = xi[NS + k];
+        ox[D.oU + NC * i] = xi[NS + 5];
+        ox[D.oU + NC * i + 1] = xi[NS + 6];
+        if (D.topt) ox[D.oTAU + i] = xi[NS + 7];
+      }
+    }
+    if (false)
+#endif
     for (int i = c.lane; i < N; i += c.width) {
       const gd* xi = X + (int64_t)i * nb;
       const int rowbase = (i == 0) ? 0 : D.eDyn + NS * (i - 1);
@@ -5264,8 +5567,14 @@ struct ObcaSolver {
     if (c.lane == 0) {
       for (int k = 0; k < 8; ++k) res.cyc[k] = cyc[k];
 #ifdef HTP_PROF_ON
+#if HTP_PROF_ON == 2   // the Riccati solve passes split: backward fill / stages, forward fill / stages; factor sub-steps
+      { const long long v[7] = {spcyc[0], spcyc[1], spcyc[2], spcyc[3], pcyc[1], pcyc[3], pcyc[5]};
+        const int slot[7] = {0, 1, 2, 3, 5, 6, 7};
+        for (int k = 0; k < 7; ++k) res.cyc[slot[k]] = v[k]; }
+#else
       for (int k = 0; k < 8; ++k)
         if (k != 4) res.cyc[k] = pcyc[k];
+#endif
 #endif
 #ifdef HTP_LPROF
       { const int slot[7] = {0, 1, 2, 3, 5, 6, 7};
@@ -5550,7 +5859,7 @@ struct ObcaSolver {
 
   // ---------------------------------------------------------- watchdog
   // stores the current point, its constraint values, the step and the reference values
-  __attribute__((noinline)) HTP_HD void start_watchdog(double th, double ph, double gbd, double dw, double dc) {
+  HTP_COLD HTP_HD void start_watchdog(double th, double ph, double gbd, double dw, double dc) {
     ls_.in_wd = 1;
     ls_.wd_th = th; ls_.wd_ph = ph; ls_.wd_gbd = gbd; ls_.wd_dw = dw; ls_.wd_dc = dc;
     ls_.wd_trial = 0;
@@ -5565,7 +5874,7 @@ struct ObcaSolver {
     if (rs) { copy_arr(A(L.wR), A(L.R), nR); copy_arr(A(L.wzR), A(L.zR), nR); copy_arr(A(L.wdR), A(L.dR), nR); }
   }
   // back to the stored point and step; its gradients, Newton rhs and the stored matrix (for SOC)
-  __attribute__((noinline)) HTP_HD void stop_watchdog() {
+  HTP_COLD HTP_HD void stop_watchdog() {
     ls_.in_wd = 0;
     copy_arr(A(L.x), A(L.wx), D.n); copy_arr(A(L.s), A(L.ws), D.md);
     copy_arr(A(L.yc), A(L.wyc), D.mc); copy_arr(A(L.yd), A(L.wyd), D.md);
@@ -5676,7 +5985,7 @@ struct ObcaSolver {
   // TrySoftRestoStep: the primal-dual step with alpha = min(primal, dual fraction to the boundary).
   // Returns 0 (rejected: nothing changed), 1 (accepted: primal-dual error reduced), 2 (accepted and
   // acceptable to the original filter criteria).  On acceptance the new iterate is in place.
-  __attribute__((noinline)) HTP_HD int try_soft_resto_step(double th, double ph, double gbd, const gd* gl) {
+  HTP_COLD HTP_HD int try_soft_resto_step(double th, double ph, double gbd, const gd* gl) {
     const gd* dx = A(L.dx); const gd* ds = A(L.ds); const gd* dyc = A(L.dyc); const gd* dyd = A(L.dyd);
     const gd* dR = A(L.dR);
     const double ap = frac_primal(dx, ds, dR);
@@ -5775,7 +6084,7 @@ struct ObcaSolver {
 
   // MinC_1NrmRestorationPhase: save the original iterate and state, set up the restoration problem
   // (RestoIterateInitializer) at the current point
-  __attribute__((noinline)) HTP_HD void enter_resto(double th, double ph, double gbd) {
+  HTP_COLD HTP_HD void enter_resto(double th, double ph, double gbd) {
     gd* osv = A(L.osv);
     ls_save(osv);
     if (c.lane == 0) { osv[24] = th; osv[25] = ph; osv[26] = gbd; osv[27] = (double)nfilt; }
@@ -5846,7 +6155,7 @@ struct ObcaSolver {
 
   // back to the original problem with x, s of the restoration phase: bound multipliers take one
   // complementarity Newton step for the whole primal change (all reset to 1 if > threshold), y = 0
-  __attribute__((noinline)) HTP_HD void leave_resto() {
+  HTP_COLD HTP_HD void leave_resto() {
     rs = false;
     const gd* osv = A(L.osv);
     ls_load(osv);
@@ -5902,7 +6211,7 @@ struct ObcaSolver {
   }
 
   // RestoRestorationPhase: n, p reset in closed form at the current x (restoration mu), zR = mu / R
-  __attribute__((noinline)) HTP_HD void resto_resto() {
+  HTP_COLD HTP_HD void resto_resto() {
     gd* ct = A(L.ct); gd* dtv = A(L.dt);
     eval_cons(A(L.x), ct, dtv);
     np_init(ct, dtv, A(L.s), mu);

@@ -75,6 +75,32 @@ struct DevWave {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
   }
 };
+
+// DevWave whose lane index and LDS bases are values the compiler rematerializes (the work-item id; the addresses
+// of module-scope __shared__ arrays, S::d() / S::i()) instead of fields of a context object.  The solver keeps a
+// reference to its context inside an object whose address escapes into out-of-line phases, so after every
+// wavefront fence (sync) each use of a field was reloaded through two dependent flat loads.  Same values: the
+// arithmetic is unchanged.  One 64-lane wavefront per workgroup (the lane is the work-item id).
+template <class S>
+struct DevWaveR : DevWave {
+  struct Lane {
+    __device__ __forceinline__ operator int() const { return (int)__builtin_amdgcn_workitem_id_x(); }
+  };
+  struct Lds {
+    __device__ __forceinline__ operator ld*() const { return S::d(); }
+  };
+  struct ILds {
+    __device__ __forceinline__ operator li*() const { return S::i(); }
+  };
+  Lane lane;
+  Lds lds;
+  ILds ildsp;
+  __device__ __forceinline__ int rank(bool pred, int& total) const {
+    const unsigned long long m = __ballot(pred ? 1 : 0);
+    total = __builtin_amdgcn_readfirstlane((int)__popcll(m));
+    return (int)__popcll(m & ((1ull << (int)lane) - 1ull));
+  }
+};
 #endif
 
 struct HostLane {

@@ -54,6 +54,8 @@ for rnd in range(2):
                         sw / max(1, r.iterations.sum()))
             if "prof" in k and "kprof" not in k:   # HTP_PROF_ON: stage-chain sub-steps (factor 1/3/5, solve 6/7)
                 nm = ["fac_relax", "fac_mfma", "fac_pn_store", "fac_chol", "total", "fac_sym", "solve_bwd*", "solve_fwd"]
+            if "sprof" in k:   # HTP_PROF_ON=2: solve passes split into ring fills and stage steps
+                nm = ["bwd_fill", "bwd_stage", "fwd_fill", "fwd_stage", "total", "fac_mfma", "fac_chol", "fac_tail"]
             line += " | " + " ".join(f"{nm[j]} {cyc[:, j].sum() / tot:.3f}" for j in (0, 1, 2, 3, 5, 6, 7))
             line += " | per-iter cycles %.3g" % (cyc[:, 4] / np.maximum(1, r.iterations)).mean()
         print(line, flush=True)
