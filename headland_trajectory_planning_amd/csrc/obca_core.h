@@ -99,6 +99,11 @@ HTP_HD inline void sincos(double x, double& s, double& c) {
 #ifndef HTP_HOIST
 #define HTP_HOIST 1
 #endif
+// pivoted local blocks: the right-hand side of each Bunch-Kaufman solve in LDS (1) or in registers via select chains
+// (0, round 5)
+#ifndef HTP_PIV_V_LDS
+#define HTP_PIV_V_LDS 1
+#endif
 // Riccati forward solve pass: Rt_i^-1 rt_i for a ring block's stages solved up front, one lane per stage (1), or
 // on the chain in each stage (0, round 5)
 #ifndef HTP_KV_HOIST
@@ -783,6 +788,132 @@ HTP_HD HTP_FI inline void bk_factor_batch(T* K, int* ip, int& neg, int& zero) {
   }
 }
 
+// Bunch-Kaufman pivot vector packed into one 64-bit word (HTP_PIV_V_LDS): entry j in bits [6 j, 6 j + 6) as
+// ip[j] + 32 (|ip[j]| <= n <= 16), so the run-time-indexed reads and writes are shifts on a register, not a
+// private-memory array.  The same integer values as bk_factor_batch's ip.
+HTP_HD HTP_FI inline unsigned long long piv_put(unsigned long long w, int j, int v) {
+  return (w & ~(63ull << (6 * j))) | ((unsigned long long)(v + 32) << (6 * j));
+}
+HTP_HD HTP_FI inline int piv_get(unsigned long long w, int j) { return (int)((w >> (6 * j)) & 63ull) - 32; }
+
+// bk_factor_batch with the pivot vector packed (piv_put)
+template <int n, int S, class T>
+HTP_HD HTP_FI inline void bk_factor_batch_p(T* K, unsigned long long& ipw, int& neg, int& zero) {
+  const double alpha = 0.6403882032022076;
+  neg = 0;
+  zero = 0;
+  ipw = 0;
+#pragma unroll
+  for (int j = 0; j < n; ++j) ipw |= 32ull << (6 * j);   // every pivot 0
+  int k = 0;
+#pragma unroll 1
+  for (int step = 0; step < n; ++step) {
+    const bool act = k < n;
+    const int kc = act ? k : 0;
+    int kstep = 1, kp = kc;
+    double cs[n];                                  // K(r, kc) for r > kc (r <= kc: in-bounds, unused)
+#pragma unroll
+    for (int r = 0; r < n; ++r) cs[r] = K[S * (r * (r + 1) / 2 + kc)];
+    const double absakk = fabs((double)K[S * (kc * (kc + 1) / 2 + kc)]);
+    int imax = kc;
+    double colmax = 0.0;
+#pragma unroll
+    for (int r = 1; r < n; ++r) {
+      const double v = fabs(cs[r]);
+      const bool t = r > kc && v > colmax;
+      colmax = t ? v : colmax;
+      imax = t ? r : imax;
+    }
+    if (act && !(absakk >= alpha * colmax) && !(absakk == 0.0 && colmax == 0.0)) {
+      double rw[n];
+#pragma unroll
+      for (int j = 0; j < n; ++j) rw[j] = fabs((double)pkx<S>(K, imax, j));
+      const double dmax = fabs((double)K[S * (imax * (imax + 1) / 2 + imax)]);
+      double rowmax = 0.0;
+#pragma unroll
+      for (int j = 0; j < n; ++j) rowmax = (j >= kc && j != imax && rw[j] > rowmax) ? rw[j] : rowmax;
+      if (absakk >= alpha * colmax * (colmax / rowmax)) kp = kc;
+      else if (dmax >= alpha * rowmax) kp = imax;
+      else { kp = imax; kstep = 2; }
+    }
+    const int kk = kc + kstep - 1;
+    if (act && kp != kk) {                         // the interchanged elements are distinct: load all, then store
+      double a[n], b[n];
+#pragma unroll
+      for (int j = 0; j < n; ++j) { a[j] = pkx<S>(K, kk, j); b[j] = pkx<S>(K, kp, j); }
+      const double dk = K[S * (kk * (kk + 1) / 2 + kk)], dp = K[S * (kp * (kp + 1) / 2 + kp)];
+#pragma unroll
+      for (int j = 0; j < n; ++j)
+        if (j >= kc && j != kk && j != kp) { pkx<S>(K, kk, j) = b[j]; pkx<S>(K, kp, j) = a[j]; }
+      K[S * (kk * (kk + 1) / 2 + kk)] = dp;
+      K[S * (kp * (kp + 1) / 2 + kp)] = dk;
+    }
+    if (act && kstep == 1) {
+      double c[n];
+#pragma unroll
+      for (int r = 0; r < n; ++r) c[r] = K[S * (r * (r + 1) / 2 + kc)];
+      double d = K[S * (kc * (kc + 1) / 2 + kc)];
+      if (d == 0.0) { zero = 1; d = 1.0; K[S * (kc * (kc + 1) / 2 + kc)] = 1.0; }
+      if (d < 0.0) ++neg;
+      const double id = 1.0 / d;
+      double lr[n];
+#pragma unroll
+      for (int r = 0; r < n; ++r) lr[r] = (r > kc) ? c[r] * id : 0.0;
+#pragma unroll
+      for (int r = 1; r < n; ++r)
+#pragma unroll
+        for (int q = 1; q <= r; ++q) {
+          T& e = K[S * (r * (r + 1) / 2 + q)];
+          const double kv = e;
+          const double nv = kv - lr[r] * c[q];
+          e = (q > kc) ? nv : kv;
+        }
+#pragma unroll
+      for (int r = 1; r < n; ++r)
+        if (r > kc) K[S * (r * (r + 1) / 2 + kc)] = c[r] * id;
+      ipw = piv_put(ipw, kc, kp);
+    } else if (act) {
+      double ca[n], cb[n];
+#pragma unroll
+      for (int r = 0; r < n; ++r) {
+        ca[r] = K[S * (r * (r + 1) / 2 + kc)];
+        cb[r] = K[S * (r * (r + 1) / 2 + (kc + 1 < n ? kc + 1 : kc))];
+      }
+      const double d11 = K[S * (kc * (kc + 1) / 2 + kc)], d21 = K[S * ((kc + 1) * (kc + 2) / 2 + kc)];
+      const double d22 = K[S * ((kc + 1) * (kc + 2) / 2 + kc + 1)];
+      const double det = d11 * d22 - d21 * d21;
+      if (det < 0.0) neg += 1;
+      else if (det > 0.0) neg += (d11 + d22 < 0.0) ? 2 : 0;
+      else zero = 1;
+      const double i11 = d22 / det, i22 = d11 / det, i21 = -d21 / det;
+      double l1[n], l2[n];
+#pragma unroll
+      for (int r = 0; r < n; ++r) {
+        const double a1 = ca[r], a2 = cb[r];
+        l1[r] = a1 * i11 + a2 * i21;
+        l2[r] = a1 * i21 + a2 * i22;
+      }
+#pragma unroll
+      for (int r = 2; r < n; ++r)
+#pragma unroll
+        for (int q = 2; q <= r; ++q) {
+          T& e = K[S * (r * (r + 1) / 2 + q)];
+          const double kv = e;
+          const double nv = kv - (l1[r] * ca[q] + l2[r] * cb[q]);
+          e = (q >= kc + 2) ? nv : kv;
+        }
+#pragma unroll
+      for (int r = 2; r < n; ++r)
+        if (r >= kc + 2) {
+          K[S * (r * (r + 1) / 2 + kc)] = l1[r];
+          K[S * (r * (r + 1) / 2 + kc + 1)] = l2[r];
+        }
+      ipw = piv_put(piv_put(ipw, kc, -(kp + 1)), kc + 1, -(kp + 1));
+    }
+    k += act ? kstep : 0;
+  }
+}
+
 template <int n, int S, class T>
 HTP_HD HTP_FI inline void bk_solve_batch(const T* K, const int* ip, double* v) {
   int k = 0;
@@ -863,6 +994,96 @@ HTP_HD HTP_FI inline void bk_solve_batch(const T* K, const int* ip, double* v) {
       sel_set<n>(v, km, t1);
       const int kp = -ipk - 1;
       if (kp != kc) { const double a = sel_get<n>(v, kc), b = sel_get<n>(v, kp); sel_set<n>(v, kc, b); sel_set<n>(v, kp, a); }
+      k -= 2;
+    }
+  }
+}
+
+// bk_solve_batch with the right-hand side in this lane's interleaved LDS slice (element j at v[64 j], HTP_PIV_V_LDS):
+// the run-time-indexed reads and writes of v (column kc, the interchanged rows) are LDS accesses instead of select
+// chains that the compiler folds into private-memory (scratch) accesses.  The same operations on the same values.
+template <int n, int S, class T, class VT>
+HTP_HD HTP_FI inline void bk_solve_batch_l(const T* K, unsigned long long ipw, VT* v) {
+  int k = 0;
+#pragma unroll 1
+  for (int step = 0; step < n; ++step) {          // forward: P, L, D
+    const bool act = k < n;
+    const int kc = act ? k : 0;
+    const int ipk = piv_get(ipw, kc);
+    const int kc1 = kc + 1 < n ? kc + 1 : kc;
+    double ca[n], cb[n];
+#pragma unroll
+    for (int r = 0; r < n; ++r) { ca[r] = K[S * (r * (r + 1) / 2 + kc)]; cb[r] = K[S * (r * (r + 1) / 2 + kc1)]; }
+    const double d11 = K[S * (kc * (kc + 1) / 2 + kc)], d21 = K[S * (kc1 * (kc1 + 1) / 2 + kc)];
+    const double d22 = K[S * (kc1 * (kc1 + 1) / 2 + kc1)];
+    if (act && ipk >= 0) {
+      const int kp = ipk;
+      if (kp != kc) { const double a = v[64 * kc], b = v[64 * kp]; v[64 * kc] = b; v[64 * kp] = a; }
+      const double vk = v[64 * kc];
+#pragma unroll
+      for (int r = 1; r < n; ++r) {
+        const double vr = v[64 * r];
+        const double nv = vr - ca[r] * vk;
+        v[64 * r] = (r > kc) ? nv : vr;
+      }
+      v[64 * kc] = v[64 * kc] / d11;
+      k += 1;
+    } else if (act) {
+      const int kp = -ipk - 1;
+      if (kp != kc + 1) {
+        const double a = v[64 * (kc + 1)], b = v[64 * kp];
+        v[64 * (kc + 1)] = b;
+        v[64 * kp] = a;
+      }
+      const double vk = v[64 * kc], vk1 = v[64 * (kc + 1)];
+#pragma unroll
+      for (int r = 2; r < n; ++r) {
+        const double vr = v[64 * r];
+        const double nv = vr - (ca[r] * vk + cb[r] * vk1);
+        v[64 * r] = (r > kc + 1) ? nv : vr;
+      }
+      const double det = d11 * d22 - d21 * d21;
+      const double b1 = vk, b2 = vk1;
+      v[64 * kc] = (d22 * b1 - d21 * b2) / det;
+      v[64 * (kc + 1)] = (-d21 * b1 + d11 * b2) / det;
+      k += 2;
+    }
+  }
+  k = n - 1;
+#pragma unroll 1
+  for (int step = 0; step < n; ++step) {          // backward: L', P'
+    const bool act = k >= 0;
+    const int kc = act ? k : 0;
+    const int ipk = piv_get(ipw, kc);
+    const int km = kc >= 1 ? kc - 1 : 0;
+    double ca[n], cm[n];
+#pragma unroll
+    for (int r = 0; r < n; ++r) { ca[r] = K[S * (r * (r + 1) / 2 + kc)]; cm[r] = K[S * (r * (r + 1) / 2 + km)]; }
+    if (act && ipk >= 0) {
+      double t = v[64 * kc];
+#pragma unroll
+      for (int r = 1; r < n; ++r) {
+        const double nt = t - ca[r] * v[64 * r];
+        t = (r > kc) ? nt : t;
+      }
+      v[64 * kc] = t;
+      const int kp = ipk;
+      if (kp != kc) { const double a = v[64 * kc], b = v[64 * kp]; v[64 * kc] = b; v[64 * kp] = a; }
+      k -= 1;
+    } else if (act) {
+      double t = v[64 * kc], t1 = v[64 * km];
+#pragma unroll
+      for (int r = 1; r < n; ++r) {
+        const double vr = v[64 * r];
+        const double nt = t - ca[r] * vr;
+        const double nt1 = t1 - cm[r] * vr;
+        t = (r > kc) ? nt : t;
+        t1 = (r > kc) ? nt1 : t1;
+      }
+      v[64 * kc] = t;
+      v[64 * km] = t1;
+      const int kp = -ipk - 1;
+      if (kp != kc) { const double a = v[64 * kc], b = v[64 * kp]; v[64 * kc] = b; v[64 * kp] = a; }
       k -= 2;
     }
   }
@@ -2026,6 +2247,37 @@ struct ObcaSolver {
     constexpr int NPK = LocalBlock<EN, EM>::NPK;
     int ip[NL];
 #if defined(__HIPCC__) || defined(HTP_EMU_WAVE)
+#if HTP_PIV_V_LDS && HTP_BK_BATCH && defined(__HIPCC__)
+    if constexpr (Ctx::kMfma && HTP_PIV_LDS && NPK <= PIV_LDS_PER_LANE) {
+      // pivots packed in a register, each right-hand side in this lane's slice of the stage-LDL scratch [0, 64 NL)
+      // (free during the local sweeps): no private-memory arrays on the pivoted path.  Device only: the host
+      // emulation keeps the register form below, the same operations on the same values (its 64 lane threads
+      // writing interleaved LDS doubles would share cache lines on every step)
+      static_assert(64 * NL <= 4 * NBMAX * NBMAX, "pivoted right-hand sides exceed the stage-LDL scratch");
+      ld* K = c.lds + RING_OFF + c.lane;
+#pragma unroll
+      for (int q = 0; q < NPK; ++q) K[64 * q] = B.K[q];
+      unsigned long long ipw;
+      bk_factor_batch_p<NL, 64>(K, ipw, inertia[0], inertia[1]);
+#if defined(HTP_LPROF) && HTP_LPROF == 2
+      lp2_t = c.clock();
+#endif
+      ld* vl = c.lds + c.lane;
+#pragma unroll
+      for (int k = 0; k < NRHS; ++k) {
+        double v[NL];
+        col(k, v, false);
+#pragma unroll
+        for (int j = 0; j < NL; ++j) vl[64 * j] = v[j];
+        bk_solve_batch_l<NL, 64>(K, ipw, vl);
+#pragma unroll
+        for (int j = 0; j < NL; ++j) v[j] = vl[64 * j];
+        col(k, v, true);
+      }
+      (void)ip;
+      return;
+    }
+#endif
     if constexpr (Ctx::kMfma && HTP_PIV_LDS && NPK <= PIV_LDS_PER_LANE) {
       ld* K = c.lds + RING_OFF + c.lane;
 #pragma unroll
