@@ -99,6 +99,11 @@ HTP_HD inline void sincos(double x, double& s, double& c) {
 #ifndef HTP_HOIST
 #define HTP_HOIST 1
 #endif
+// local sweeps: the trip loops' bound and lane index read once before the loop (1), or in every trip (0, round 5;
+// each re-read is a pointer chain from the solver object issued behind the previous trip's stores)
+#ifndef HTP_HOIST_TRIP
+#define HTP_HOIST_TRIP 1
+#endif
 // pivoted local blocks: the right-hand side of each Bunch-Kaufman solve in LDS (1) or in registers via select chains
 // (0, round 5)
 #ifndef HTP_PIV_V_LDS
@@ -2469,8 +2474,13 @@ struct ObcaSolver {
 #ifdef HTP_LPROF
     long long lt0 = c.clock(), lscan = 0;
 #endif
-    for (int b0 = 0; b0 < D.P; b0 += c.width) {
-      const int p = b0 + c.lane;
+#if HTP_HOIST_TRIP
+    const int nblk_ = c.uniform_i(D.P), lane_ = c.lane;   // loop bound and lane read once, not behind every trip's stores
+#else
+    const int nblk_ = D.P, lane_ = 0;
+#endif
+    for (int b0 = 0; b0 < (HTP_HOIST_TRIP ? nblk_ : D.P); b0 += c.width) {
+      const int p = b0 + (HTP_HOIST_TRIP ? lane_ : (int)c.lane);
       bool piv = false;
       HTP_LP1(2, 1);
       if (p < D.P) {
@@ -2543,7 +2553,7 @@ struct ObcaSolver {
     HTP_LP(6, 1);
 #endif
     for (int b0 = 0; b0 < npiv; b0 += c.width) {
-      const int q = b0 + c.lane;
+      const int q = b0 + (HTP_HOIST_TRIP ? lane_ : (int)c.lane);
       HTP_LP1(3, 1);
       if (q < npiv) {
         const int p = (int)PL[q];
@@ -2632,8 +2642,13 @@ struct ObcaSolver {
       local_rhs_out<EN, EM>(p, B, v, q3, PR);
     };
     int npiv = 0;
-    for (int b0 = 0; b0 < D.P; b0 += c.width) {
-      const int p = b0 + c.lane;
+#if HTP_HOIST_TRIP
+    const int nblk_ = c.uniform_i(D.P), lane_ = c.lane;   // loop bound and lane read once, not behind every trip's stores
+#else
+    const int nblk_ = D.P, lane_ = 0;
+#endif
+    for (int b0 = 0; b0 < (HTP_HOIST_TRIP ? nblk_ : D.P); b0 += c.width) {
+      const int p = b0 + (HTP_HOIST_TRIP ? lane_ : (int)c.lane);
       bool piv = false;
       if (p < D.P) {
         LocalBlock<EN, EM> B;
@@ -2658,7 +2673,7 @@ struct ObcaSolver {
     }
     c.sync();
     for (int b0 = 0; b0 < npiv; b0 += c.width) {
-      const int q = b0 + c.lane;
+      const int q = b0 + (HTP_HOIST_TRIP ? lane_ : (int)c.lane);
       if (q < npiv) {
         const int p = (int)PL[q];
         LocalBlock<EN, EM> B;
@@ -2736,8 +2751,13 @@ struct ObcaSolver {
       os[2 * p + 1] = (bs3 + y3) / B.Ds3;
     };
     int npiv = 0;
-    for (int b0 = 0; b0 < D.P; b0 += c.width) {
-      const int p = b0 + c.lane;
+#if HTP_HOIST_TRIP
+    const int nblk_ = c.uniform_i(D.P), lane_ = c.lane;   // loop bound and lane read once, not behind every trip's stores
+#else
+    const int nblk_ = D.P, lane_ = 0;
+#endif
+    for (int b0 = 0; b0 < (HTP_HOIST_TRIP ? nblk_ : D.P); b0 += c.width) {
+      const int p = b0 + (HTP_HOIST_TRIP ? lane_ : (int)c.lane);
       bool piv = false;
       if (p < D.P) {
         LocalBlock<EN, EM> B;
@@ -2762,7 +2782,7 @@ struct ObcaSolver {
     }
     c.sync();
     for (int b0 = 0; b0 < npiv; b0 += c.width) {
-      const int q = b0 + c.lane;
+      const int q = b0 + (HTP_HOIST_TRIP ? lane_ : (int)c.lane);
       if (q < npiv) {
         const int p = (int)PL[q];
         LocalBlock<EN, EM> B;
