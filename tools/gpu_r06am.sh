@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 6 (am): config E and the 4096 slice on the final binary
+# slice of the 8-GPU share (config D 4096, 20 and 6 steps)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+( while true; do date >> gpurun_out/heartbeat.log; sleep 30; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+timeout -k 10 400 python3 -u bench.py --batch 4096 --steps 20 --no-cpu-baseline > gpurun_out/r06am_slice4096_s20.json 2> gpurun_out/r06am_slice4096_s20.log &&
+timeout -k 10 300 python3 -u bench.py --batch 4096 --steps 6 --no-cpu-baseline > gpurun_out/r06am_slice4096_s6.json 2> gpurun_out/r06am_slice4096_s6.log &&
+timeout -k 10 900 python3 -u bench.py --config E --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/r06am_benchE.json 2> gpurun_out/r06am_benchE.log
